@@ -1,0 +1,153 @@
+/* fedcodec.h — C ABI of the MI355X-native gradient codec (libfedcodec.so, gfx950).
+ *
+ * Replaces the NumPy kernels inside OpenMSFTL's ftl/compression + FedAVG hot path:
+ *   Compression.compress          ftl/compression/compression.py:23-77
+ *     'top'              -> fc_topk_encode (+ fc_topk_encode_exact)   compression.py:31-37
+ *     'rand'             -> fc_topk_encode (key_mode = PHILOX, native) or
+ *                           fc_mask_encode (host permutation mask, parity)  compression.py:39-45
+ *     'dropout-biased'   -> fc_mask_encode (codec = DROPOUT_BIASED)   compression.py:47-53
+ *     'dropout-unbiased' -> fc_mask_encode (codec = DROPOUT_UNBIASED) compression.py:55-60
+ *     dense result       -> fc_decode_dense
+ *   Aggregator.aggregate_grads G build   aggregation.py:61-63   -> fc_decode_accumulate
+ *   GAR.weighted_average / FedAvg        gar.py:32-46, 53-56    -> fc_decode_accumulate /
+ *                                                                  fc_weighted_sum_dense
+ * The reference has no FFI of its own (100 % Python): these entry points are
+ * what its Python layer binds through ctypes.
+ *
+ * Conventions: every pointer is a DEVICE pointer unless stated; buffers are caller-owned;
+ * calls are stream-ordered and asynchronous; nothing allocates (scratch lives in the caller's
+ * workspace); return 0 on success, <0 on argument / HIP errors (fc_last_error() explains,
+ * thread-local).  Device-side outcomes (e.g. the sampled bracket missing) are reported in the
+ * packet header's `status`, read by the host after the stream is synchronised.
+ */
+#ifndef FEDCODEC_H_
+#define FEDCODEC_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* fc_stream_t; /* hipStream_t */
+
+#define FC_ABI_VERSION 1
+
+/* return codes */
+#define FC_OK 0
+#define FC_ERR_ARG (-1)
+#define FC_ERR_HIP (-2)
+#define FC_ERR_WORKSPACE (-3)
+
+/* packet header status (device-written) */
+#define FC_STATUS_OK 0
+#define FC_STATUS_RETRY_EXACT 1   /* sampled bracket missed: call fc_topk_encode_exact */
+#define FC_STATUS_OVERFLOW 2      /* more entries than the packet capacity */
+#define FC_STATUS_TIMEOUT 3       /* a bounded device spin expired (never expected) */
+
+/* codecs (compression_function) */
+#define FC_CODEC_TOP 1
+#define FC_CODEC_RAND 2
+#define FC_CODEC_DROPOUT_BIASED 3
+#define FC_CODEC_DROPOUT_UNBIASED 4
+
+/* key sources for fc_topk_encode */
+#define FC_KEY_MAGNITUDE 0   /* |g| (top-k) */
+#define FC_KEY_PHILOX 1      /* Philox4x32-10 word per element (native rand-k) */
+
+/* packet formats */
+#define FC_FMT_IDXVAL 0      /* uint32 idx[] ascending + float val[] */
+#define FC_FMT_BITMAP 1      /* uint32 bitmap[ceil(N/8192)*256] + float val[] */
+
+#define FC_CHUNK 8192        /* elements per chunk (directory granularity) */
+
+/* Device-resident packet header (96 bytes). */
+typedef struct fc_packet_hdr {
+  uint64_t thresh;      /* T64: entry kept iff (key<<index_bits | idx) >= thresh      */
+  uint64_t lower;       /* L64: every element with comp >= lower is listed             */
+  uint32_t n;           /* gradient length                                             */
+  uint32_t k;           /* coordinates kept by the codec (top/rand)                    */
+  uint32_t n_entries;   /* entries written to idx/val (>= k: sampled-bracket slack)    */
+  uint32_t index_bits;  /* IB = max(1, ceil(log2 n))                                   */
+  uint32_t codec;       /* FC_CODEC_*                                                  */
+  uint32_t status;      /* FC_STATUS_*                                                 */
+  uint32_t n_definite;  /* diagnostics: elements above the bracket                     */
+  uint32_t n_cand;      /* diagnostics: elements inside the bracket                    */
+  uint64_t seed;        /* Philox key (native RNG modes)                               */
+  uint64_t offset;      /* Philox counter high words                                   */
+  double p;             /* dropout probability (unbiased scale 1/p applied at decode)  */
+  uint32_t chunk;       /* FC_CHUNK                                                    */
+  uint32_t format;      /* FC_FMT_*                                                    */
+  uint32_t key_mode;    /* FC_KEY_* (top/rand)                                         */
+  uint32_t reserved[3];
+} fc_packet_hdr;
+
+/* One packet as seen by the decoders (host- or device-resident array element, 48 bytes). */
+typedef struct fc_packet_view {
+  const uint32_t* idx;          /* FC_FMT_IDXVAL                        */
+  const float* val;
+  const uint32_t* bitmap;       /* FC_FMT_BITMAP                        */
+  const uint32_t* dir;          /* ceil(N/FC_CHUNK)+1 entry offsets     */
+  const fc_packet_hdr* hdr;
+  float weight;                 /* FedAVG weight w_i (gar.py:37-44)     */
+  uint32_t reserved;
+} fc_packet_view;
+
+int fc_abi_version(void);
+const char* fc_last_error(void);
+
+/* ---- sizes ------------------------------------------------------------------------- */
+uint64_t fc_num_chunks(uint64_t n);
+size_t fc_workspace_bytes(uint64_t n);        /* scratch for one encoder (one stream)   */
+uint64_t fc_topk_capacity(uint64_t n, uint64_t k); /* idx/val entries a top packet needs */
+/* zero a freshly allocated workspace once (self-cleaning afterwards) */
+int fc_workspace_init(void* ws, size_t ws_bytes, fc_stream_t stream);
+
+/* ---- encode: top-k / native rand-k (compression.py:31-45) ---------------------------
+ * Single streaming read of g: a sampled bracket [t_lo, t_hi] is estimated from a
+ * stratified sample, every element with key >= t_lo is compacted in index order (decoupled
+ * look-back, one launch), then the exact k-th composite key is resolved from the bracket's
+ * candidates.  hdr->status == FC_STATUS_RETRY_EXACT means the bracket missed (adversarial
+ * data): call fc_topk_encode_exact with the same arguments. */
+int fc_topk_encode(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_t seed,
+                   uint64_t offset, uint32_t* idx, float* val, uint64_t capacity,
+                   uint32_t* dir, fc_packet_hdr* hdr, void* ws, size_t ws_bytes,
+                   fc_stream_t stream);
+/* Exact radix-select path (several reads of g); always succeeds; n_entries == k. */
+int fc_topk_encode_exact(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_t seed,
+                         uint64_t offset, uint32_t* idx, float* val, uint64_t capacity,
+                         uint32_t* dir, fc_packet_hdr* hdr, void* ws, size_t ws_bytes,
+                         fc_stream_t stream);
+
+/* ---- encode: mask codecs (compression.py:39-60) -------------------------------------
+ * codec = FC_CODEC_DROPOUT_* or FC_CODEC_RAND (parity mode: mask from the host's
+ * np.random.permutation).  mask_bits (little-endian bit i = element i, N/32 words) is the
+ * host-drawn mask in parity mode; NULL selects native Philox Bernoulli(p) keyed by seed.
+ * format: FC_FMT_BITMAP (bitmap required) or FC_FMT_IDXVAL (idx required). */
+int fc_mask_encode(const float* g, uint64_t n, int codec, const uint32_t* mask_bits,
+                   double p, uint64_t seed, uint64_t offset, int format, uint32_t* idx,
+                   float* val, uint32_t* bitmap, uint64_t capacity, uint32_t* dir,
+                   fc_packet_hdr* hdr, void* ws, size_t ws_bytes, fc_stream_t stream);
+
+/* ---- decode (compression.py dense result) --------------------------------------------
+ * pkt: HOST pointer to one view.  out is float (out_f64 = 0) or double (out_f64 = 1; the
+ * reference's float64 dropout result, compression.py:52/60). */
+int fc_decode_dense(const fc_packet_view* pkt, int format, uint64_t n, void* out, int out_f64,
+                    fc_stream_t stream);
+
+/* ---- FedAVG over packets (aggregation.py:61-63 + gar.py:44), bit-exact fp32 ----------
+ * views: DEVICE array of m views (same format), client order = row order of G.
+ * acc[j] = fl(w_0 * d_0[j]);  acc[j] = fl(acc[j] + fl(w_i * d_i[j])) for i = 1..m-1. */
+int fc_decode_accumulate(const fc_packet_view* views_dev, int m, int format, uint64_t n,
+                         float* acc, fc_stream_t stream);
+
+/* ---- FedAVG over dense rows (gar.py:44 for 'full'): rows = DEVICE array of m row
+ * pointers, w = DEVICE fp32[m]. */
+int fc_weighted_sum_dense(const float* const* rows, const float* w, int m, uint64_t n,
+                          float* out, fc_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FEDCODEC_H_ */

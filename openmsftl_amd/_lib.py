@@ -1,0 +1,108 @@
+"""ctypes binding of libfedcodec.so (include/fedcodec.h).
+
+The library is the ONLY compute path: if it is missing or fails to load, every call raises
+``FedCodecUnavailable`` — there is deliberately no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libfedcodec.so")
+
+# --- constants mirrored from include/fedcodec.h --------------------------------------
+FC_OK = 0
+FC_STATUS_OK, FC_STATUS_RETRY_EXACT, FC_STATUS_OVERFLOW, FC_STATUS_TIMEOUT = 0, 1, 2, 3
+FC_CODEC_TOP, FC_CODEC_RAND, FC_CODEC_DROPOUT_BIASED, FC_CODEC_DROPOUT_UNBIASED = 1, 2, 3, 4
+FC_KEY_MAGNITUDE, FC_KEY_PHILOX = 0, 1
+FC_FMT_IDXVAL, FC_FMT_BITMAP = 0, 1
+FC_CHUNK = 8192
+HDR_BYTES = 96
+
+
+class FedCodecError(RuntimeError):
+    """A C-ABI call returned an error code (message from fc_last_error())."""
+
+
+class FedCodecUnavailable(RuntimeError):
+    """libfedcodec.so is not built / not loadable: the HIP path is mandatory."""
+
+
+class PacketHdr(ctypes.Structure):
+    _fields_ = [("thresh", ctypes.c_uint64), ("lower", ctypes.c_uint64),
+                ("n", ctypes.c_uint32), ("k", ctypes.c_uint32),
+                ("n_entries", ctypes.c_uint32), ("index_bits", ctypes.c_uint32),
+                ("codec", ctypes.c_uint32), ("status", ctypes.c_uint32),
+                ("n_definite", ctypes.c_uint32), ("n_cand", ctypes.c_uint32),
+                ("seed", ctypes.c_uint64), ("offset", ctypes.c_uint64),
+                ("p", ctypes.c_double), ("chunk", ctypes.c_uint32),
+                ("format", ctypes.c_uint32), ("key_mode", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32 * 3)]
+
+
+class PacketView(ctypes.Structure):
+    _fields_ = [("idx", ctypes.c_void_p), ("val", ctypes.c_void_p),
+                ("bitmap", ctypes.c_void_p), ("dir", ctypes.c_void_p),
+                ("hdr", ctypes.c_void_p), ("weight", ctypes.c_float),
+                ("reserved", ctypes.c_uint32)]
+
+
+assert ctypes.sizeof(PacketHdr) == HDR_BYTES
+assert ctypes.sizeof(PacketView) == 48
+
+_u64, _i32, _sz, _vp, _dbl = (ctypes.c_uint64, ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p,
+                              ctypes.c_double)
+
+#: every entry point declared in include/fedcodec.h: name -> (restype, argtypes)
+SIGNATURES = {
+    "fc_abi_version": (_i32, []),
+    "fc_last_error": (ctypes.c_char_p, []),
+    "fc_num_chunks": (_u64, [_u64]),
+    "fc_workspace_bytes": (_sz, [_u64]),
+    "fc_topk_capacity": (_u64, [_u64, _u64]),
+    "fc_workspace_init": (_i32, [_vp, _sz, _vp]),
+    "fc_topk_encode": (_i32, [_vp, _u64, _u64, _i32, _u64, _u64, _vp, _vp, _u64, _vp, _vp,
+                              _vp, _sz, _vp]),
+    "fc_topk_encode_exact": (_i32, [_vp, _u64, _u64, _i32, _u64, _u64, _vp, _vp, _u64, _vp,
+                                    _vp, _vp, _sz, _vp]),
+    "fc_mask_encode": (_i32, [_vp, _u64, _i32, _vp, _dbl, _u64, _u64, _i32, _vp, _vp, _vp,
+                              _u64, _vp, _vp, _vp, _sz, _vp]),
+    "fc_decode_dense": (_i32, [ctypes.POINTER(PacketView), _i32, _u64, _vp, _i32, _vp]),
+    "fc_decode_accumulate": (_i32, [_vp, _i32, _i32, _u64, _vp, _vp]),
+    "fc_weighted_sum_dense": (_i32, [_vp, _vp, _i32, _u64, _vp, _vp]),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+def load(path: str = LIB_PATH):
+    """Load and declare libfedcodec.so (torch is imported first: one HIP runtime)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        import torch  # noqa: F401  (binds libamdhip64.so.7 from torch before our .so)
+        if not os.path.exists(path):
+            raise FedCodecUnavailable(
+                f"{path} not built — run `python -m openmsftl_amd.build` (hipcc, gfx950)")
+        try:
+            lib = ctypes.CDLL(path)
+        except OSError as e:
+            raise FedCodecUnavailable(f"cannot load {path}: {e}") from e
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.fc_abi_version() != 1:
+            raise FedCodecUnavailable("libfedcodec.so ABI mismatch")
+        _lib = lib
+        return lib
+
+
+def check(rc: int, what: str):
+    if rc != FC_OK:
+        msg = load().fc_last_error()
+        raise FedCodecError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")

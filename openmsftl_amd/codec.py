@@ -1,0 +1,265 @@
+"""Device-resident codec API over libfedcodec.so (torch tensors in HBM, torch's stream).
+
+    pkt = encode_top(g, k)                 # compression.py:31-37   (one read of g)
+    pkt = encode_rand_philox(g, k, seed)   # compression.py:39-45   native RNG
+    pkt = encode_mask(g, codec, p, ...)    # compression.py:47-60 / rand parity
+    q   = decode(pkt)                      # the dense vector compress() returns
+    agg = decode_accumulate(pkts, w)       # aggregation.py:61-63 + gar.py:44, bit-exact fp32
+
+Packets live on the GPU: ``idx``/``val`` (or ``bitmap``/``val``), a per-8192-element chunk
+directory ``dir`` and a 96-byte device header (include/fedcodec.h ``fc_packet_hdr``).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib as L
+
+_U32 = torch.int32  # uint32 payloads are stored in int32 tensors (bit-identical)
+
+
+def _vp(t: Optional[torch.Tensor]):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _stream(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _require_cuda_f32(g: torch.Tensor, name="g"):
+    if not isinstance(g, torch.Tensor) or not g.is_cuda:
+        raise TypeError(f"{name} must be a CUDA (HIP) tensor")
+    if g.dtype != torch.float32:
+        raise TypeError(f"{name} must be float32 (got {g.dtype}); the HIP codec is fp32-only")
+    if g.dim() != 1 or not g.is_contiguous():
+        raise ValueError(f"{name} must be a contiguous 1-D tensor")
+    if g.data_ptr() % 16:
+        raise ValueError(f"{name} must be 16-byte aligned")
+
+
+# ---------------------------------------------------------------------------------------
+class Workspace:
+    """Per-(device, stream) encoder scratch (self-cleaning after one memset)."""
+
+    _cache: dict = {}
+
+    def __init__(self, n: int, device: torch.device):
+        lib = L.load()
+        self.n = n
+        self.nbytes = int(lib.fc_workspace_bytes(n))
+        self.buf = torch.empty(self.nbytes, dtype=torch.uint8, device=device)
+        L.check(lib.fc_workspace_init(_vp(self.buf), self.nbytes, _stream(device)),
+                "fc_workspace_init")
+
+    @classmethod
+    def get(cls, n: int, device: torch.device) -> "Workspace":
+        key = (device.index if device.index is not None else torch.cuda.current_device(),
+               torch.cuda.current_stream(device).cuda_stream)
+        ws = cls._cache.get(key)
+        if ws is None or ws.n < n:
+            ws = cls(n, device)
+            cls._cache[key] = ws
+        return ws
+
+
+@dataclass
+class Packet:
+    """A compressed gradient resident in HBM (see include/fedcodec.h)."""
+    n: int
+    fmt: int
+    val: torch.Tensor
+    dir: torch.Tensor
+    hdr: torch.Tensor                      # uint8[96] (may be a row of a batch tensor)
+    idx: Optional[torch.Tensor] = None
+    bitmap: Optional[torch.Tensor] = None
+    k: int = 0
+
+    @classmethod
+    def alloc(cls, n: int, fmt: int, capacity: int, device, hdr: Optional[torch.Tensor] = None,
+              k: int = 0) -> "Packet":
+        lib = L.load()
+        nch = int(lib.fc_num_chunks(n))
+        cap = max(int(capacity), 4)
+        return cls(n=n, fmt=fmt, k=k,
+                   val=torch.empty(cap, dtype=torch.float32, device=device),
+                   dir=torch.empty(nch + 1, dtype=_U32, device=device),
+                   hdr=hdr if hdr is not None else torch.empty(L.HDR_BYTES, dtype=torch.uint8,
+                                                               device=device),
+                   idx=torch.empty(cap, dtype=_U32, device=device) if fmt == L.FC_FMT_IDXVAL else None,
+                   bitmap=torch.empty(nch * 256, dtype=_U32, device=device)
+                   if fmt == L.FC_FMT_BITMAP else None)
+
+    @property
+    def capacity(self) -> int:
+        return self.val.numel()
+
+    def view(self, weight: float = 1.0) -> L.PacketView:
+        return L.PacketView(idx=self.idx.data_ptr() if self.idx is not None else 0,
+                            val=self.val.data_ptr(),
+                            bitmap=self.bitmap.data_ptr() if self.bitmap is not None else 0,
+                            dir=self.dir.data_ptr(), hdr=self.hdr.data_ptr(),
+                            weight=float(np.float32(weight)), reserved=0)
+
+    def header(self) -> L.PacketHdr:
+        """Synchronous D2H read of the device header."""
+        raw = self.hdr.cpu().numpy().tobytes()
+        return L.PacketHdr.from_buffer_copy(raw)
+
+    def raw_entries(self):
+        """(idx uint32, val float32, header) of every LISTED entry, ascending — includes the
+        sampled-bracket slack (comp < thresh); inspection / test helper (synchronises)."""
+        h = self.header()
+        ne = h.n_entries
+        val = self.val[:ne].cpu().numpy()
+        if self.fmt == L.FC_FMT_IDXVAL:
+            idx = self.idx[:ne].cpu().numpy().view(np.uint32)
+        else:
+            bits = np.unpackbits(self.bitmap.cpu().numpy().view(np.uint8), bitorder="little")
+            idx = np.nonzero(bits[: self.n])[0].astype(np.uint32)
+        return idx, val, h
+
+
+def headers(packets: Sequence[Packet]) -> list:
+    """Read many device headers with one synchronising copy when they share storage."""
+    return [p.header() for p in packets]
+
+
+# ---------------------------------------------------------------------------------------
+def encode_top(g: torch.Tensor, k: int, *, key_mode: int = L.FC_KEY_MAGNITUDE, seed: int = 0,
+               offset: int = 0, packet: Optional[Packet] = None,
+               check: bool = True, exact: bool = False) -> Packet:
+    """Top-k (|g|) or native rand-k (Philox keys) into an idx/val packet.
+
+    ``check=True`` synchronises, reads the header and falls back to the exact device path
+    if the sampled bracket missed (FC_STATUS_RETRY_EXACT).  With ``check=False`` call
+    :func:`resolve` on the batch later (one sync per batch)."""
+    _require_cuda_f32(g)
+    lib = L.load()
+    n = g.numel()
+    if not 0 <= k <= n:
+        raise ValueError(f"k={k} outside [0, {n}]")
+    ws = Workspace.get(n, g.device)
+    if packet is None:
+        cap = int(lib.fc_topk_capacity(n, k))
+        packet = Packet.alloc(n, L.FC_FMT_IDXVAL, cap, g.device, k=k)
+    packet.k = k
+    fn = lib.fc_topk_encode_exact if exact else lib.fc_topk_encode
+    L.check(fn(_vp(g), n, k, key_mode, seed, offset, _vp(packet.idx), _vp(packet.val),
+               packet.capacity, _vp(packet.dir), _vp(packet.hdr), _vp(ws.buf), ws.nbytes,
+               _stream(g.device)), "fc_topk_encode")
+    packet._enc = (g, k, key_mode, seed, offset)
+    if check:
+        resolve([packet])
+    return packet
+
+
+def resolve(packets: Sequence[Packet]) -> int:
+    """Re-encode (exact path) every top/rand packet whose sampled bracket missed.
+    Returns the number of packets that needed the exact path."""
+    lib = L.load()
+    redo = 0
+    for p in packets:
+        h = p.header()
+        if h.status == L.FC_STATUS_OK:
+            continue
+        if h.status != L.FC_STATUS_RETRY_EXACT or not hasattr(p, "_enc"):
+            raise L.FedCodecError(f"packet status {h.status}")
+        g, k, key_mode, seed, offset = p._enc
+        ws = Workspace.get(g.numel(), g.device)
+        L.check(lib.fc_topk_encode_exact(_vp(g), g.numel(), k, key_mode, seed, offset,
+                                         _vp(p.idx), _vp(p.val), p.capacity, _vp(p.dir),
+                                         _vp(p.hdr), _vp(ws.buf), ws.nbytes,
+                                         _stream(g.device)), "fc_topk_encode_exact")
+        redo += 1
+        h2 = p.header()
+        if h2.status != L.FC_STATUS_OK:
+            raise L.FedCodecError(f"exact encode status {h2.status}")
+    return redo
+
+
+def encode_mask(g: torch.Tensor, codec: int, *, p: float = 0.5,
+                mask_bits: Optional[torch.Tensor] = None, seed: int = 0, offset: int = 0,
+                fmt: int = L.FC_FMT_BITMAP, packet: Optional[Packet] = None,
+                capacity: Optional[int] = None) -> Packet:
+    """Mask codecs: dropout-biased / dropout-unbiased (Philox or host mask) and rand-k with a
+    host-drawn permutation mask (parity mode).  ``mask_bits``: int32 device tensor, bit i of
+    word i//32 = element i."""
+    _require_cuda_f32(g)
+    lib = L.load()
+    n = g.numel()
+    ws = Workspace.get(n, g.device)
+    if mask_bits is not None and (mask_bits.dtype != _U32 or not mask_bits.is_cuda
+                                  or mask_bits.numel() * 32 < n):
+        raise ValueError("mask_bits must be an int32 CUDA tensor of ceil(n/32) words")
+    if packet is None:
+        packet = Packet.alloc(n, fmt, capacity if capacity is not None else n, g.device)
+    L.check(lib.fc_mask_encode(_vp(g), n, codec, _vp(mask_bits), float(p), seed, offset, fmt,
+                               _vp(packet.idx), _vp(packet.val), _vp(packet.bitmap),
+                               packet.capacity, _vp(packet.dir), _vp(packet.hdr), _vp(ws.buf),
+                               ws.nbytes, _stream(g.device)), "fc_mask_encode")
+    return packet
+
+
+def decode(packet: Packet, out: Optional[torch.Tensor] = None,
+           dtype: torch.dtype = torch.float32) -> torch.Tensor:
+    """Dense reconstruction (the array compress() returns)."""
+    lib = L.load()
+    dev = packet.val.device
+    if out is None:
+        out = torch.empty(packet.n, dtype=dtype, device=dev)
+    if out.dtype not in (torch.float32, torch.float64) or out.numel() != packet.n:
+        raise ValueError("out must be float32/float64 with n elements")
+    v = packet.view()
+    L.check(lib.fc_decode_dense(ctypes.byref(v), packet.fmt, packet.n, _vp(out),
+                                int(out.dtype == torch.float64), _stream(dev)),
+            "fc_decode_dense")
+    return out
+
+
+def views_tensor(packets: Sequence[Packet], weights, device) -> torch.Tensor:
+    """Device array of fc_packet_view (client order = G row order)."""
+    arr = (L.PacketView * len(packets))(*[p.view(w) for p, w in zip(packets, weights)])
+    host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+    return host.to(device)
+
+
+def decode_accumulate(packets: Sequence[Packet], weights, out: Optional[torch.Tensor] = None,
+                      views: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """FedAVG over packets: bit-exact ``np.sum(G * w[:, None], axis=0)`` (gar.py:44)."""
+    lib = L.load()
+    if not packets:
+        raise ValueError("no packets")
+    fmt, n, dev = packets[0].fmt, packets[0].n, packets[0].val.device
+    if any(p.fmt != fmt or p.n != n for p in packets):
+        raise ValueError("packets must share n and format")
+    if out is None:
+        out = torch.empty(n, dtype=torch.float32, device=dev)
+    if views is None:
+        views = views_tensor(packets, weights, dev)
+    L.check(lib.fc_decode_accumulate(_vp(views), len(packets), fmt, n, _vp(out), _stream(dev)),
+            "fc_decode_accumulate")
+    return out
+
+
+def weighted_sum_dense(rows, weights: torch.Tensor, out: Optional[torch.Tensor] = None):
+    """gar.py:44 on dense device rows (a (M, N) tensor or a list of 1-D tensors)."""
+    lib = L.load()
+    if isinstance(rows, torch.Tensor):
+        rows = list(rows.unbind(0))
+    for r in rows:
+        _require_cuda_f32(r, "row")
+    n, dev = rows[0].numel(), rows[0].device
+    if any(r.numel() != n for r in rows):
+        raise ValueError("rows must have equal length")
+    w = weights.to(device=dev, dtype=torch.float32).contiguous()
+    ptrs = torch.tensor([r.data_ptr() for r in rows], dtype=torch.int64).to(dev)
+    if out is None:
+        out = torch.empty(n, dtype=torch.float32, device=dev)
+    L.check(lib.fc_weighted_sum_dense(_vp(ptrs), _vp(w), len(rows), n, _vp(out), _stream(dev)),
+            "fc_weighted_sum_dense")
+    return out

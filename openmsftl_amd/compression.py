@@ -1,0 +1,140 @@
+"""Drop-in for OpenMSFTL's ``ftl.compression.Compression`` (compression.py:8-77), on MI355X.
+
+Same constructor keys and defaults, same ``compress(grad, layer_wise=False)`` contract:
+  * 'full'              returns the caller's object itself            (compression.py:27-29)
+  * 'top'               fresh array, input dtype, k = round(f*N)      (compression.py:31-37)
+  * 'rand'              fresh array, input dtype                      (compression.py:39-45)
+  * 'dropout-biased'    float64 result                                (compression.py:47-53)
+  * 'dropout-unbiased'  float64 result, fl64(g)/p                     (compression.py:55-60)
+  * 'qsgd', unknown names, layer_wise=True -> NotImplementedError at call time (:24,62,76)
+The compute runs in hand-written HIP kernels (libfedcodec.so); there is no CPU fallback.
+
+RNG: by default ('rng': 'numpy') 'rand'/'dropout-*' draw from the process-global legacy
+``np.random`` exactly as the reference (same calls, same stream consumption), and only the
+mask/index set crosses to the GPU.  ``'rng': 'philox'`` draws on the device instead
+(Philox4x32-10 keyed by ``'seed'``, counter advanced per call) — no host RNG work, not
+stream-identical to the reference (documented in DESIGN.md).
+
+Inputs: 1-D float32 NumPy arrays (the reference's `client.grad`, client.py:53) or 1-D
+float32 CUDA tensors (device-resident; the result is then a CUDA tensor).
+
+Deliberate, documented deviations:
+  * ties in 'top' are broken highest-index-first (= stable argsort reversed); the
+    reference's unstable argsort leaves that choice implementation-defined;
+  * for 'dropout-*' a dropped coordinate is +0.0 where the reference writes g*0 (-0.0 for
+    negative g); numerically equal, and inf/NaN inputs still give NaN as in the reference.
+"""
+from __future__ import annotations
+
+from typing import Dict
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from . import codec
+
+
+def kept_count(fraction: float, n: int) -> int:
+    """``round(f * N)`` (compression.py:34/42) and the slice semantics of ``idx[:k]``."""
+    k = round(fraction * n)
+    return len(range(n)[:k])
+
+
+def bitmask_words(indices_or_mask: np.ndarray, n: int, is_mask: bool) -> np.ndarray:
+    """Little-endian bit mask (bit i of word i//32) from an index list or a 0/1 mask."""
+    words = (n + 31) // 32
+    bits = np.zeros(words * 32, dtype=bool)
+    if is_mask:
+        bits[:n] = indices_or_mask != 0
+    else:
+        bits[indices_or_mask] = True
+    return np.packbits(bits, bitorder="little").view(np.uint32)
+
+
+class Compression:
+    def __init__(self, compression_config: Dict):
+        # compression.py:18-21 — verbatim keys and defaults, no validation
+        self.compression_function = compression_config.get("compression_function", 'full')
+        self.num_bits = compression_config.get("num_bits", 8)
+        self.fraction_coordinates = compression_config.get("fraction_coordinate", 0.5)
+        self.dropout_p = compression_config.get("dropout_p", 0.5)
+        # extensions (optional keys; defaults = reference behaviour)
+        self.rng = compression_config.get("rng", "numpy")
+        self.seed = int(compression_config.get("seed", 0))
+        self.device = compression_config.get("device", None)
+        self._calls = 0
+
+    # ------------------------------------------------------------------------------------
+    def compress(self, grad, layer_wise=False):
+        if layer_wise:
+            raise NotImplementedError
+        fn = self.compression_function
+        if fn == 'full':
+            return grad
+        if fn not in ('top', 'rand', 'dropout-biased', 'dropout-unbiased'):
+            raise NotImplementedError          # 'qsgd' (:62-64) and unknown names (:76-77)
+        L.load()                               # the HIP path is mandatory
+        on_device = isinstance(grad, torch.Tensor)
+        n = int(grad.shape[0])
+        if fn in ('top', 'rand'):
+            k = kept_count(self.fraction_coordinates, n)
+            host_idx = None
+            if fn == 'rand' and self.rng == 'numpy':
+                host_idx = np.random.permutation(n)[:k]          # compression.py:43
+            if n == 0:
+                return grad.clone() if on_device else np.zeros_like(grad)
+            g = self._to_device(grad)
+            if fn == 'top':
+                pkt = codec.encode_top(g, k)
+            elif host_idx is not None:
+                mask = torch.from_numpy(bitmask_words(host_idx, n, False).view(np.int32)).to(g.device)
+                pkt = codec.encode_mask(g, L.FC_CODEC_RAND, mask_bits=mask, fmt=L.FC_FMT_IDXVAL,
+                                        capacity=max(k, 1))
+            else:
+                pkt = codec.encode_top(g, k, key_mode=L.FC_KEY_PHILOX, seed=self.seed,
+                                       offset=self._next_offset())
+            out = codec.decode(pkt)
+            return out if on_device else out.cpu().numpy()
+        # dropout-* ---------------------------------------------------------------------
+        p = self.dropout_p
+        host_mask = None
+        if self.rng == 'numpy':
+            host_mask = np.random.binomial(1, p, (n,))            # compression.py:51/58
+        elif not (0.0 <= p <= 1.0):
+            raise ValueError("p < 0, p > 1 or p is NaN")
+        if n == 0:
+            return (torch.zeros(0, dtype=torch.float64, device=grad.device) if on_device
+                    else np.zeros(0, dtype=np.float64))
+        g = self._to_device(grad)
+        codec_id = L.FC_CODEC_DROPOUT_BIASED if fn == 'dropout-biased' else L.FC_CODEC_DROPOUT_UNBIASED
+        if host_mask is not None:
+            mask = torch.from_numpy(bitmask_words(host_mask, n, True).view(np.int32)).to(g.device)
+            pkt = codec.encode_mask(g, codec_id, p=float(p), mask_bits=mask)
+        else:
+            pkt = codec.encode_mask(g, codec_id, p=float(p), seed=self.seed,
+                                    offset=self._next_offset())
+        hdr = pkt.header()
+        if hdr.status != L.FC_STATUS_OK:
+            raise L.FedCodecError(f"mask encode status {hdr.status}")
+        out = codec.decode(pkt, dtype=torch.float64)               # reference returns float64
+        return out if on_device else out.cpu().numpy()
+
+    # ------------------------------------------------------------------------------------
+    def _next_offset(self) -> int:
+        self._calls += 1
+        return self._calls
+
+    def _to_device(self, grad) -> torch.Tensor:
+        if isinstance(grad, torch.Tensor):
+            if grad.dim() != 1:
+                raise ValueError("compress expects a 1-D gradient (client.py:53 flat vector)")
+            return grad.contiguous()
+        a = np.asarray(grad)
+        if a.ndim != 1:
+            raise ValueError("compress expects a 1-D gradient (client.py:53 flat vector)")
+        if a.dtype != np.float32:
+            raise TypeError(f"HIP codec handles float32 gradients (got {a.dtype}); "
+                            "see DESIGN.md §Scope")
+        dev = torch.device(self.device) if self.device else torch.device("cuda")
+        return torch.from_numpy(np.ascontiguousarray(a)).to(dev)

@@ -1,0 +1,172 @@
+// fc_common.h — shared device helpers for the MI355X (gfx950) gradient codec.
+//
+// Geometry: every streaming kernel works on CHUNKs of 8192 fp32 elements (32 KiB) with a
+// 256-thread workgroup (4 waves of 64).  Inside a chunk, element e is owned by
+//     iteration i = e / 1024, wave w = (e / 256) % 4, lane l = (e / 4) % 64, slot j = e % 4
+// so each wave instruction moves 1 KiB contiguous (one float4 per lane) and the (i, w, l, j)
+// order is exactly ascending index order — ballots + mbcnt give ordered compaction offsets
+// with no block-wide scan per element.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fc {
+
+constexpr int kBlock = 256;                 // threads per workgroup
+constexpr int kWaves = kBlock / 64;
+constexpr int kVec = 8;                     // float4 per thread per chunk
+constexpr int kChunk = kBlock * 4 * kVec;   // 8192 elements
+constexpr int kChunkWords = kChunk / 32;    // bitmap words per chunk (256)
+constexpr int kHistBits = 12;
+constexpr int kHistBins = 1 << kHistBits;   // 4096
+constexpr int kSmallCap = 2048;             // exact-finish list (LDS bitonic)
+constexpr int kEngineGrid = 256;            // radix-engine workgroups (one per CU)
+constexpr int kEnginePasses = 6;            // ceil(63 / 12): enough for any comp width
+
+constexpr uint32_t kNanKey = 0x7f800001u;   // every NaN sorts above +inf
+constexpr uint64_t kSelectNothing = 1ull << 63;
+
+// ---- status granules (decoupled look-back) -------------------------------------------
+// [63:34] epoch (30 bits) | [33:32] flag | [31:0] value
+constexpr uint64_t kFlagAgg = 1, kFlagInc = 2;
+__device__ __forceinline__ uint64_t granule(uint32_t epoch, uint64_t flag, uint32_t v) {
+  return ((uint64_t)(epoch & 0x3fffffffu) << 34) | (flag << 32) | v;
+}
+__device__ __forceinline__ uint32_t g_epoch(uint64_t s) { return (uint32_t)(s >> 34); }
+__device__ __forceinline__ uint32_t g_flag(uint64_t s) { return (uint32_t)(s >> 32) & 3u; }
+__device__ __forceinline__ uint32_t g_val(uint64_t s) { return (uint32_t)s; }
+
+template <typename T>
+__device__ __forceinline__ T ld_agent(const T* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ void st_agent(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ---- keys ----------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t mag_key(float x) {
+  uint32_t u = __float_as_uint(x) & 0x7fffffffu;
+  return u > 0x7f800000u ? kNanKey : u;
+}
+__device__ __forceinline__ uint64_t comp_of(uint32_t key, uint32_t idx, uint32_t ib) {
+  return ((uint64_t)key << ib) | idx;
+}
+
+// ---- Philox4x32-10 (Salmon et al. SC'11); KAT-pinned by oracle/philox.py -------------
+__device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+    const uint32_t lo0 = c.x * 0xD2511F53u, hi0 = __umulhi(c.x, 0xD2511F53u);
+    const uint32_t lo1 = c.z * 0xCD9E8D57u, hi1 = __umulhi(c.z, 0xCD9E8D57u);
+    c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
+  }
+  return c;
+}
+// the four words for elements 4b .. 4b+3
+__device__ __forceinline__ uint4 philox_block(uint64_t b, uint64_t seed, uint64_t offset) {
+  return philox4x32_10(make_uint4((uint32_t)b, (uint32_t)(b >> 32), (uint32_t)offset,
+                                  (uint32_t)(offset >> 32)),
+                       (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+__device__ __forceinline__ uint32_t philox_word(uint64_t i, uint64_t seed, uint64_t offset) {
+  const uint4 r = philox_block(i >> 2, seed, offset);
+  const uint32_t s = (uint32_t)(i & 3);
+  return s == 0 ? r.x : s == 1 ? r.y : s == 2 ? r.z : r.w;
+}
+
+// Key source: MAG = |g| bit pattern (top-k); PHILOX = random word (native rand-k).
+enum KeyMode : int { kKeyMag = 0, kKeyPhilox = 1 };
+
+// ---- wave helpers --------------------------------------------------------------------
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+__device__ __forceinline__ uint32_t prefix_count(uint64_t mask) {   // popc(mask & lanemask_lt)
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                   __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// float4 load of elements [e, e+4) with zero fill past n (16-B aligned base required)
+__device__ __forceinline__ float4 load4(const float* __restrict__ g, uint64_t e, uint64_t n) {
+  if (e + 4 <= n) return *reinterpret_cast<const float4*>(g + e);
+  float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (e + 0 < n) r.x = g[e + 0];
+  if (e + 1 < n) r.y = g[e + 1];
+  if (e + 2 < n) r.z = g[e + 2];
+  if (e + 3 < n) r.w = g[e + 3];
+  return r;
+}
+__device__ __forceinline__ float f4get(const float4& v, int j) {
+  return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w;
+}
+__device__ __forceinline__ void f4set(float4& v, int j, float x) {
+  if (j == 0) v.x = x; else if (j == 1) v.y = x; else if (j == 2) v.z = x; else v.w = x;
+}
+
+// Spread the 8 bits of x to bits 0,4,8,...,28 (bitmap assembly from 4 ballots).
+__device__ __forceinline__ uint32_t spread4(uint32_t x) {
+  x &= 0xffu;
+  x = (x | (x << 12)) & 0x000F000Fu;
+  x = (x | (x << 6)) & 0x03030303u;
+  x = (x | (x << 3)) & 0x11111111u;
+  return x;
+}
+
+// Exclusive block scan of one value per thread (256 threads).
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_tmp,
+                                                    uint32_t* total) {
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  uint32_t inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += t;
+  }
+  if (lane == 63) s_tmp[w] = inc;
+  __syncthreads();
+  uint32_t base = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < kWaves; ++i) {
+    const uint32_t s = s_tmp[i];
+    if (i < w) base += s;
+    tot += s;
+  }
+  __syncthreads();
+  if (total) *total = tot;
+  return base + inc - v;
+}
+
+// Workgroup "last arriver" ticket (MI355X_MICROARCH.md §visibility valid producer form):
+// every storing wave drains, barrier, lane 0 releases at agent scope, drains, then adds.
+// Returns true in every thread of the last-arriving workgroup, after an agent acquire.
+__device__ __forceinline__ bool last_block_arrive(uint32_t* counter, uint32_t nblocks,
+                                                  uint32_t* s_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t t = atomicAdd(counter, 1u);
+    const bool last = (t == nblocks - 1);
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *s_flag = last ? 1u : 0u;
+  }
+  __syncthreads();
+  return *s_flag != 0;
+}
+
+}  // namespace fc

@@ -1,0 +1,85 @@
+// fc_state.h — encoder workspace layout + kernel argument blocks (device and host views).
+#pragma once
+#include <stdint.h>
+#include "../../include/fedcodec.h"
+#include "fc_common.h"
+
+namespace fc {
+
+// Per-encoder state.  Self-cleaning: every counter a kernel consumes is reset by the
+// last-arriving workgroup of the launch that consumed it, so a stream of encodes (or a
+// graph replay) needs the workspace zeroed only once (fc_workspace_init).
+struct alignas(16) TopkState {
+  uint64_t ticket;       // k_compact chunk tickets {epoch:32 | count:32}; the holder of the
+                         // last ticket starts the next epoch at count 0
+  uint64_t L64;          // entries written: comp >= L64
+  uint64_t e_prefix;     // radix engine: resolved high bits of T64
+  uint32_t err;          // sticky device error (spin timeout)
+  uint32_t a_done, b_done;
+  uint32_t b1_hi, b1_lo; // level-1 sample bins of the two bracket ranks
+  uint32_t rr_hi, rr_lo; // residual 1-based ranks inside those bins
+  uint32_t hi_none, lo_all;
+  uint32_t t_lo, t_hi;   // bracket (keys): list key >= t_lo; definite key > t_hi
+  uint32_t cand_on, n_hi, n_cand, cand_over, ent_over;
+  uint32_t e_shift, e_rank, e_matched, e_done, e_src, e_ticket, e_small_n, e_status;
+};
+static_assert(sizeof(TopkState) <= 256, "state block");
+
+struct WsLayout {
+  uint64_t nchunks, cand_cap;
+  uint64_t off_hist1, off_hist2h, off_hist2l, off_ehist, off_small, off_status, off_cand, bytes;
+  __host__ __device__ static WsLayout of(uint64_t n) {
+    WsLayout L;
+    L.nchunks = (n + kChunk - 1) / kChunk;
+    L.cand_cap = n / 32 > 65536 ? n / 32 : 65536;
+    uint64_t o = 256;
+    L.off_hist1 = o;  o += 4ull * kHistBins;
+    L.off_hist2h = o; o += 4ull * kHistBins;
+    L.off_hist2l = o; o += 4ull * kHistBins;
+    L.off_ehist = o;  o += 4ull * kHistBins;
+    L.off_small = o;  o += 8ull * kSmallCap;
+    L.off_status = o; o += 8ull * (L.nchunks ? L.nchunks : 1);
+    L.off_cand = o;   o += 8ull * L.cand_cap;
+    L.bytes = (o + 255) & ~255ull;
+    return L;
+  }
+};
+
+struct HdrInit {          // static header fields, written by the first kernel of a pipeline
+  uint64_t seed, offset;
+  double p;
+  uint32_t n, k, ib, codec, format, key_mode;
+};
+
+struct WsPtrs {
+  TopkState* st;
+  uint32_t *hist1, *hist2h, *hist2l, *ehist;
+  uint64_t *small, *status, *cand;
+  uint64_t cand_cap;
+};
+
+__device__ __forceinline__ void write_hdr_static(fc_packet_hdr* h, const HdrInit& hi) {
+  h->thresh = 0; h->lower = 0;
+  h->n = hi.n; h->k = hi.k; h->n_entries = 0; h->index_bits = hi.ib;
+  h->codec = hi.codec; h->status = FC_STATUS_OK; h->n_definite = 0; h->n_cand = 0;
+  h->seed = hi.seed; h->offset = hi.offset; h->p = hi.p;
+  h->chunk = kChunk; h->format = hi.format; h->key_mode = hi.key_mode;
+  h->reserved[0] = h->reserved[1] = h->reserved[2] = 0;
+}
+
+// Sampling plan (host-computed, passed by value).
+struct SamplePlan {
+  uint64_t n;
+  uint32_t nseg;       // 1024-element segments
+  uint32_t full;       // 1: segments tile [0, n) exactly (n <= kFullSampleMax)
+  int64_t r_hi, r_lo;  // 1-based ranks from the top inside the sample
+  uint32_t hi_none, lo_all;
+};
+constexpr uint64_t kFullSampleMax = 1ull << 20;
+
+__device__ __forceinline__ uint64_t seg_start(const SamplePlan& P, uint32_t s) {
+  if (P.full || P.nseg == 1) return (uint64_t)s * 1024;
+  return ((uint64_t)s * (P.n - 1024) / (P.nseg - 1)) & ~3ull;
+}
+
+}  // namespace fc

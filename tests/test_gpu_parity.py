@@ -1,0 +1,305 @@
+"""GPU parity: the HIP codec (through the C ABI) against the CPU oracle / reference goldens.
+
+Run on an MI355X:  python -m pytest tests -m gpu -x -q
+Bars: index sets and top/rand values bit-exact; dropout values equal as the reference's
+consumers see them (assert_array_equal: NaN==NaN, +0==-0) and bit-exact on every nonzero
+finite coordinate; FedAVG bit-exact fp32.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+from conftest import golden, has_tie_at_boundary
+from oracle import compression_oracle as co
+from oracle import gar_oracle as go
+from oracle import packet_oracle as po
+from oracle import philox as ph
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+G = golden()
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from openmsftl_amd import _lib
+    lib = _lib.load()
+    assert lib.fc_abi_version() == 1
+
+
+def _codec():
+    from openmsftl_amd import codec
+    return codec
+
+
+def _L():
+    from openmsftl_amd import _lib
+    return _lib
+
+
+def _gpu_topk(g_np, k, exact=False):
+    codec = _codec()
+    g = torch.from_numpy(np.ascontiguousarray(g_np, dtype=np.float32)).cuda()
+    pkt = codec.encode_top(g, k, exact=exact)
+    out = codec.decode(pkt).cpu().numpy()
+    return pkt, out
+
+
+def _check_top_packet(g_np, k, pkt, out):
+    keys = po.mag_key(g_np)
+    want_idx = po.selected_indices(keys, k)
+    want_out = po.decode_dense(g_np.shape[0], want_idx, g_np[want_idx])
+    assert out.tobytes() == want_out.tobytes()
+    idx, val, h = pkt.raw_entries()
+    assert h.status == 0
+    assert np.all(np.diff(idx.astype(np.int64)) > 0), "packet indices must ascend"
+    assert np.uint64(h.thresh) == po.threshold(keys, k)
+    c = po.comps(keys)[idx]
+    kept = c >= np.uint64(h.thresh)
+    np.testing.assert_array_equal(idx[kept], want_idx)
+    assert val.tobytes() == g_np[idx].tobytes()
+    assert h.n_entries >= k and kept.sum() == k
+
+
+# ---- top: golden cases ----------------------------------------------------------------
+@pytest.mark.parametrize("name", G.cases("top__"))
+def test_top_golden(name):
+    from openmsftl_amd import Compression
+    m = G.meta(name)
+    g = G.input(name)
+    C = Compression({"compression_function": "top", "fraction_coordinate": m["fraction"]})
+    out = C.compress(g.copy())
+    ora = co.compress({"compression_function": "top", "fraction_coordinate": m["fraction"]}, g)
+    assert out.dtype == np.float32
+    assert out.tobytes() == ora.tobytes()
+    k = co.effective_k(co.num_kept(m["fraction"], g.shape[0]), g.shape[0])
+    if not has_tie_at_boundary(g, k):
+        assert out.tobytes() == G.arr(name, "output").tobytes()   # the reference itself
+
+
+# ---- top: sizes, fractions, fast vs exact ----------------------------------------------
+SIZES = [1, 5, 4095, 4096, 8191, 8192, 8193, 100_003, 1 << 20, (1 << 20) + 17, 3_000_001]
+FRACS = [0.1, 0.01, 0.5, 0.9, 1e-6, 0.999]
+
+
+@pytest.mark.parametrize("n", SIZES)
+@pytest.mark.parametrize("f", FRACS)
+def test_top_sizes(n, f):
+    g = np.random.default_rng(n * 7 + int(f * 1000)).standard_normal(n, dtype=np.float32)
+    g *= np.float32(10.0) ** np.random.default_rng(n).uniform(-4, 1, n).astype(np.float32)
+    k = co.effective_k(co.num_kept(f, n), n)
+    pkt, out = _gpu_topk(g, k)
+    _check_top_packet(g, k, pkt, out)
+
+
+@pytest.mark.parametrize("n,f", [(100_003, 0.1), (3_000_001, 0.01), (1 << 20, 0.37)])
+def test_top_exact_path_equals_fast(n, f):
+    g = np.random.default_rng(5).standard_normal(n, dtype=np.float32)
+    k = co.effective_k(co.num_kept(f, n), n)
+    p1, o1 = _gpu_topk(g, k)
+    p2, o2 = _gpu_topk(g, k, exact=True)
+    assert o1.tobytes() == o2.tobytes()
+    idx2, _, h2 = p2.raw_entries()
+    assert h2.n_entries == k
+    _check_top_packet(g, k, p2, o2)
+
+
+ADVERSARIAL = {
+    "constant": lambda n: np.full(n, 0.5, np.float32),
+    "zeros_signed": lambda n: np.where(np.arange(n) % 3 == 0, -0.0, 0.0).astype(np.float32),
+    "ascending": lambda n: np.arange(n, dtype=np.float32),
+    "smallint_ties": lambda n: np.random.default_rng(1).integers(-4, 5, n).astype(np.float32),
+    "nan_inf_mix": lambda n: np.where(np.random.default_rng(2).random(n) < 0.05, np.nan,
+                                      np.where(np.random.default_rng(3).random(n) < 0.05,
+                                               -np.inf, np.random.default_rng(4).standard_normal(n))
+                                      ).astype(np.float32),
+    "denormals": lambda n: (np.random.default_rng(6).standard_normal(n) * 1e-41).astype(np.float32),
+    "layered_scales": lambda n: (np.random.default_rng(8).standard_normal(n)
+                                 * np.repeat(10.0 ** np.arange(-6, 2), -(-n // 8))[:n]).astype(np.float32),
+}
+
+
+@pytest.mark.parametrize("kind", sorted(ADVERSARIAL))
+@pytest.mark.parametrize("n", [70_001, 2_500_000])
+@pytest.mark.parametrize("f", [0.1, 0.5])
+def test_top_adversarial(kind, n, f):
+    g = ADVERSARIAL[kind](n)
+    k = co.effective_k(co.num_kept(f, n), n)
+    pkt, out = _gpu_topk(g, k)
+    _check_top_packet(g, k, pkt, out)
+
+
+def test_top_bracket_miss_falls_back_to_exact():
+    """Large values hidden between the sampled segments -> bracket misses -> exact path."""
+    n = 4 << 20
+    g = np.zeros(n, np.float32)
+    nseg = max(64, min(1024, n // 32 // 1024))
+    starts = ((np.arange(nseg, dtype=np.int64) * (n - 1024)) // (nseg - 1)) & ~3
+    sampled = np.zeros(n, bool)
+    for s in starts:
+        sampled[s:s + 1024] = True
+    hidden = np.nonzero(~sampled)[0]
+    g[hidden[: n // 8]] = np.random.default_rng(0).standard_normal(n // 8).astype(np.float32)
+    k = n // 10
+    codec = _codec()
+    gt = torch.from_numpy(g).cuda()
+    pkt = codec.encode_top(gt, k, check=False)
+    torch.cuda.synchronize()
+    redo = codec.resolve([pkt])
+    assert redo == 1
+    out = codec.decode(pkt).cpu().numpy()
+    _check_top_packet(g, k, pkt, out)
+
+
+@pytest.mark.parametrize("key", sorted(G.manifest["large"]))
+def test_top_large_digests(key):
+    d = G.manifest["large"][key]
+    g = np.random.default_rng(d["seed"]).standard_normal(d["n"], dtype=np.float32)
+    pkt, out = _gpu_topk(g, d["k"])
+    assert hashlib.sha256(out.tobytes()).hexdigest() == d["output_sha256"]
+    idx, val, h = pkt.raw_entries()
+    kept = po.comps(po.mag_key(g))[idx] >= np.uint64(h.thresh)
+    assert hashlib.sha256(idx[kept].tobytes()).hexdigest() == d["sorted_idx_sha256"]
+
+
+def test_top_128M_properties():
+    """BASELINE size: 134,217,728 fp32, f = 0.1 — size-independent properties."""
+    n, f = 134_217_728, 0.1
+    k = co.num_kept(f, n)
+    codec = _codec()
+    gen = torch.Generator(device="cuda").manual_seed(1234)
+    g = torch.randn(n, device="cuda", generator=gen)
+    pkt = codec.encode_top(g, k)
+    out = codec.decode(pkt)
+    h = pkt.header()
+    assert h.status == 0 and h.n_entries >= k
+    nz = out != 0
+    assert int(nz.sum()) == k
+    assert torch.equal(out[nz], g[nz])                       # exact copies
+    a = g.abs()
+    assert float(a[nz].min()) >= float(a[~nz].max())         # every kept >= every dropped
+    idx = pkt.idx[: h.n_entries].to(torch.int64)
+    assert bool((idx[1:] > idx[:-1]).all())                  # ascending packet
+    # slack stays small (the packet carries few unselected entries)
+    assert h.n_entries - k < 0.06 * k
+
+
+# ---- rand ------------------------------------------------------------------------------
+@pytest.mark.parametrize("name", G.cases("rand__"))
+def test_rand_numpy_rng_golden(name):
+    from openmsftl_amd import Compression
+    m = G.meta(name)
+    g = G.input(name)
+    np.random.seed(m["seed"])
+    out = Compression({"compression_function": "rand",
+                       "fraction_coordinate": m["fraction"]}).compress(g)
+    assert int(np.random.randint(0, 2**31 - 1)) == m["rng_next"]
+    assert out.dtype == np.float32
+    assert out.tobytes() == G.arr(name, "output").tobytes()
+
+
+@pytest.mark.parametrize("n,f", [(1000, 0.1), (100_003, 0.5), (3_000_001, 0.01)])
+def test_rand_philox_matches_oracle(n, f):
+    codec = _codec()
+    L = _L()
+    g = np.random.default_rng(n).standard_normal(n, dtype=np.float32)
+    k = co.num_kept(f, n)
+    seed, off = 0xDEADBEEF12345, 7
+    pkt = codec.encode_top(torch.from_numpy(g).cuda(), k, key_mode=L.FC_KEY_PHILOX,
+                           seed=seed, offset=off)
+    out = codec.decode(pkt).cpu().numpy()
+    keys = (ph.element_words(n, seed, off) >> np.uint32(1)).astype(np.uint32)
+    want = po.selected_indices(keys, k)
+    assert out.tobytes() == po.decode_dense(n, want, g[want]).tobytes()
+
+
+# ---- dropout ---------------------------------------------------------------------------
+def _dropout_equal(out, ref):
+    assert out.dtype == np.float64 == ref.dtype
+    np.testing.assert_array_equal(out, ref)                 # NaN==NaN, +0==-0
+    fin = np.isfinite(ref) & (ref != 0)
+    assert out[fin].tobytes() == ref[fin].tobytes()
+
+
+@pytest.mark.parametrize("name", G.cases("dropout-"))
+def test_dropout_numpy_rng_golden(name):
+    from openmsftl_amd import Compression
+    m = G.meta(name)
+    g = G.input(name)
+    np.random.seed(m["seed"])
+    out = Compression({"compression_function": m["codec"], "dropout_p": m["p"]}).compress(g)
+    if "rng_next" in m:
+        assert int(np.random.randint(0, 2**31 - 1)) == m["rng_next"]
+    _dropout_equal(out, G.arr(name, "output"))
+
+
+@pytest.mark.parametrize("codec_name", ["dropout-biased", "dropout-unbiased"])
+@pytest.mark.parametrize("p", [0.1, 0.3, 1.0, 0.0])
+def test_dropout_philox_matches_oracle(codec_name, p):
+    codec = _codec()
+    L = _L()
+    n = 1_000_003
+    g = np.random.default_rng(11).standard_normal(n, dtype=np.float32)
+    g[::9973] = np.inf
+    seed, off = 42, 3
+    cid = L.FC_CODEC_DROPOUT_BIASED if codec_name == "dropout-biased" else L.FC_CODEC_DROPOUT_UNBIASED
+    pkt = codec.encode_mask(torch.from_numpy(g).cuda(), cid, p=p, seed=seed, offset=off)
+    out = codec.decode(pkt, dtype=torch.float64).cpu().numpy()
+    mask = ph.bernoulli_mask(n, p, seed, off).astype(np.int64)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        ref = g * mask if codec_name == "dropout-biased" else (g * mask) / p
+    _dropout_equal(out, ref)
+    out32 = codec.decode(pkt).cpu().numpy()
+    with np.errstate(invalid="ignore"):
+        np.testing.assert_array_equal(out32, ref.astype(np.float32))
+
+
+# ---- FedAVG ----------------------------------------------------------------------------
+@pytest.mark.parametrize("name", G.cases("fedavg__"))
+def test_fedavg_dense_golden(name):
+    from openmsftl_amd import FedAvg
+    Gm = G.arr(name, "G")
+    out = FedAvg({"aggregation_scheme": "fed_avg"}).aggregate(Gm)
+    assert out.tobytes() == G.arr(name, "output").tobytes()
+
+
+@pytest.mark.parametrize("M,n,f", [(4, 4096, 0.1), (17, 100_003, 0.1), (64, 70_001, 0.01)])
+def test_fedavg_packets_bit_exact(M, n, f):
+    """Packets -> k_decode<ACC> == reference FedAvg on the dense G of the same rows."""
+    codec = _codec()
+    from openmsftl_amd import FedAvg
+    rng = np.random.default_rng(M)
+    grads = [(rng.standard_normal(n) * 10.0 ** rng.uniform(-4, -1)).astype(np.float32)
+             for _ in range(M)]
+    k = co.num_kept(f, n)
+    pkts = [codec.encode_top(torch.from_numpy(x).cuda(), k) for x in grads]
+    agg = FedAvg({}).aggregate_packets(pkts).cpu().numpy()
+    Gd = go.build_dense_G([co.compress({"compression_function": "top",
+                                        "fraction_coordinate": f}, x) for x in grads], np.float32)
+    ref = go.FedAvgOracle({}).aggregate(Gd)
+    assert agg.tobytes() == ref.tobytes()
+
+
+def test_fedavg_packets_dropout_unbiased_and_weights():
+    codec = _codec()
+    L = _L()
+    M, n, p = 9, 50_001, 0.1
+    rng = np.random.default_rng(3)
+    grads = [rng.standard_normal(n).astype(np.float32) for _ in range(M)]
+    w = rng.uniform(-1, 1, M).astype(np.float32)
+    pkts, rows = [], []
+    for i, x in enumerate(grads):
+        pk = codec.encode_mask(torch.from_numpy(x).cuda(), L.FC_CODEC_DROPOUT_UNBIASED, p=p,
+                               seed=100 + i)
+        pkts.append(pk)
+        mask = ph.bernoulli_mask(n, p, 100 + i).astype(np.int64)
+        rows.append(((x * mask) / p).astype(np.float32))
+    agg = codec.decode_accumulate(pkts, list(w)).cpu().numpy()
+    ref = go.sequential_weighted_sum(rows, w)
+    np.testing.assert_array_equal(agg, ref)
+    nz = ref != 0
+    assert agg[nz].tobytes() == ref[nz].tobytes()
