@@ -147,6 +147,17 @@ int fc_decode_accumulate(const fc_packet_view* views_dev, int m, int format, uin
 int fc_weighted_sum_dense(const float* const* rows, const float* w, int m, uint64_t n,
                           float* out, fc_stream_t stream);
 
+/* ---- measurement: HIP events around selected kernels, on the stream they run on -------
+ * mask: FC_TIME_* bits.  Between fc_timing_begin and fc_timing_end every launch of a
+ * selected kernel class is bracketed by a hipEvent pair; fc_timing_end synchronises those
+ * events and returns per-class total milliseconds and launch counts (arrays of 4). */
+#define FC_TIME_COMPACT 1    /* k_compact: the single streaming pass over g (encode)   */
+#define FC_TIME_DECODE 2     /* k_decode: dense decode / FedAVG decode-accumulate      */
+#define FC_TIME_ENGINE 4     /* k_engine: exact threshold resolution                   */
+#define FC_TIME_SAMPLE 8     /* k_sample: bracket estimation                           */
+int fc_timing_begin(uint32_t mask);
+int fc_timing_end(double* total_ms, uint64_t* launches);
+
 #ifdef __cplusplus
 }
 #endif

@@ -72,7 +72,37 @@ SIGNATURES = {
     "fc_decode_dense": (_i32, [ctypes.POINTER(PacketView), _i32, _u64, _vp, _i32, _vp]),
     "fc_decode_accumulate": (_i32, [_vp, _i32, _i32, _u64, _vp, _vp]),
     "fc_weighted_sum_dense": (_i32, [_vp, _vp, _i32, _u64, _vp, _vp]),
+    "fc_timing_begin": (_i32, [ctypes.c_uint32]),
+    "fc_timing_end": (_i32, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)]),
 }
+
+FC_TIME_COMPACT, FC_TIME_DECODE, FC_TIME_ENGINE, FC_TIME_SAMPLE = 1, 2, 4, 8
+TIME_CLASSES = ("compact", "decode", "engine", "sample")
+
+
+class KernelTimer:
+    """HIP-event timing of selected kernel classes on the stream they are launched on."""
+
+    def __init__(self, mask: int = 0xF):
+        self.mask = mask
+        self.ms = {}
+        self.launches = {}
+
+    def __enter__(self):
+        check(load().fc_timing_begin(self.mask), "fc_timing_begin")
+        return self
+
+    def __exit__(self, *exc):
+        ms = (ctypes.c_double * 4)()
+        n = (ctypes.c_uint64 * 4)()
+        check(load().fc_timing_end(ms, n), "fc_timing_end")
+        self.ms = {c: ms[i] for i, c in enumerate(TIME_CLASSES)}
+        self.launches = {c: int(n[i]) for i, c in enumerate(TIME_CLASSES)}
+        return False
+
+    def avg_us(self, cls: str) -> float:
+        n = self.launches.get(cls, 0)
+        return 1e3 * self.ms[cls] / n if n else float("nan")
 
 _lock = threading.Lock()
 _lib = None

@@ -31,15 +31,15 @@ def _stream(device=None):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
-def _require_cuda_f32(g: torch.Tensor, name="g"):
+def _require_cuda_f32(g: torch.Tensor, name="g", align: int = 16):
     if not isinstance(g, torch.Tensor) or not g.is_cuda:
         raise TypeError(f"{name} must be a CUDA (HIP) tensor")
     if g.dtype != torch.float32:
         raise TypeError(f"{name} must be float32 (got {g.dtype}); the HIP codec is fp32-only")
     if g.dim() != 1 or not g.is_contiguous():
         raise ValueError(f"{name} must be a contiguous 1-D tensor")
-    if g.data_ptr() % 16:
-        raise ValueError(f"{name} must be 16-byte aligned")
+    if g.data_ptr() % align:
+        raise ValueError(f"{name} must be {align}-byte aligned")
 
 
 # ---------------------------------------------------------------------------------------
@@ -252,7 +252,7 @@ def weighted_sum_dense(rows, weights: torch.Tensor, out: Optional[torch.Tensor] 
     if isinstance(rows, torch.Tensor):
         rows = list(rows.unbind(0))
     for r in rows:
-        _require_cuda_f32(r, "row")
+        _require_cuda_f32(r, "row", align=4)
     n, dev = rows[0].numel(), rows[0].device
     if any(r.numel() != n for r in rows):
         raise ValueError("rows must have equal length")

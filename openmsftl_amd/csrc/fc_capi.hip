@@ -1,9 +1,12 @@
 // fc_capi.hip — extern "C" entry points of libfedcodec.so (declared in include/fedcodec.h).
 // Argument checking, sampling plans and launch sequences; no allocation, no host syncs.
 #include <math.h>
+#include <stdlib.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
+
+#include <vector>
 
 // Part of the unity build (fedcodec.hip): the kernels and their argument structs from
 // fc_topk.hip / fc_decode.hip are visible here.
@@ -90,8 +93,36 @@ static int check_common(const float* g, uint64_t n, void* ws, size_t ws_bytes) {
   return FC_OK;
 }
 
+// ---- opt-in kernel timing (fc_timing_begin / fc_timing_end) ------------------------------
+namespace {
+struct EvPair { hipEvent_t a, b; uint32_t cat; };
+std::vector<EvPair> g_ev;
+size_t g_ev_used = 0;
+uint32_t g_time_mask = 0;
+
+// Brackets one launch with a hipEvent pair on its own stream when its class is selected.
+struct TimedLaunch {
+  long slot = -1;
+  hipStream_t s;
+  TimedLaunch(uint32_t cat, hipStream_t s_) : s(s_) {
+    if (!(g_time_mask & cat)) return;
+    if (g_ev_used == g_ev.size()) {
+      EvPair e{nullptr, nullptr, 0};
+      if (hipEventCreate(&e.a) != hipSuccess || hipEventCreate(&e.b) != hipSuccess) return;
+      g_ev.push_back(e);
+    }
+    slot = (long)g_ev_used++;
+    g_ev[slot].cat = cat;
+    (void)hipEventRecord(g_ev[slot].a, s);
+  }
+  ~TimedLaunch() { if (slot >= 0) (void)hipEventRecord(g_ev[slot].b, s); }
+};
+}  // namespace
+
 static int launch_engine(int key_mode, const EngineArgs& base, int passes, hipStream_t s) {
+  if (const char* dbg = getenv("FC_DEBUG_ENGINE_PASSES")) passes = atoi(dbg);  // debugging only
   for (int p = 0; p < passes; ++p) {
+    TimedLaunch t(FC_TIME_ENGINE, s);
     EngineArgs a = base;
     a.first = p == 0;
     if (key_mode == FC_KEY_PHILOX) hipLaunchKernelGGL(k_engine<kKeyPhilox>, dim3(kEngineGrid), dim3(kBlock), 0, s, a);
@@ -102,6 +133,7 @@ static int launch_engine(int key_mode, const EngineArgs& base, int passes, hipSt
 }
 
 static int launch_compact_key(int key_mode, const CompactArgs& a, hipStream_t s) {
+  TimedLaunch t(FC_TIME_COMPACT, s);
   if (key_mode == FC_KEY_PHILOX)
     hipLaunchKernelGGL((k_compact<kKeyPhilox, kPredKey, FC_FMT_IDXVAL>), dim3(a.nchunks), dim3(kBlock), 0, s, a);
   else
@@ -129,6 +161,32 @@ uint64_t fc_topk_capacity(uint64_t n, uint64_t k) {
   const double slack = (2.0 * (6.0 * sqrt(S * q * (1.0 - q)) + 16.0) + 2048.0) / S * (double)n;
   uint64_t cap = k + (uint64_t)(1.5 * slack) + 65536;
   return cap > n ? n : cap;
+}
+
+int fc_timing_begin(uint32_t mask) {
+  g_time_mask = mask;
+  g_ev_used = 0;
+  return FC_OK;
+}
+
+int fc_timing_end(double* total_ms, uint64_t* launches) {
+  FC_CHECK(total_ms && launches, "NULL argument");
+  for (int c = 0; c < 4; ++c) { total_ms[c] = 0.0; launches[c] = 0; }
+  int rc = FC_OK;
+  for (size_t i = 0; i < g_ev_used; ++i) {
+    float ms = 0.f;
+    if (hipEventSynchronize(g_ev[i].b) != hipSuccess ||
+        hipEventElapsedTime(&ms, g_ev[i].a, g_ev[i].b) != hipSuccess) {
+      rc = fail(FC_ERR_HIP, "timing events failed");
+      continue;
+    }
+    const int c = __builtin_ctz(g_ev[i].cat);
+    total_ms[c] += ms;
+    launches[c] += 1;
+  }
+  g_time_mask = 0;
+  g_ev_used = 0;
+  return rc;
 }
 
 int fc_workspace_init(void* ws, size_t ws_bytes, fc_stream_t stream) {
@@ -194,6 +252,8 @@ int fc_topk_encode(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_
   hipStream_t s = (hipStream_t)stream;
   const SamplePlan P = make_plan(n, k);
   const uint32_t sgrid = P.nseg < 1024 ? P.nseg : 1024;
+  {
+  TimedLaunch t(FC_TIME_SAMPLE, s);
   if (key_mode == FC_KEY_PHILOX) {
     hipLaunchKernelGGL((k_sample<kKeyPhilox, 1>), dim3(sgrid), dim3(kBlock), 0, s, g, P, seed, offset, ca.W, ca.ib, hdr, hi);
     FC_LAUNCHED("k_sample1");
@@ -204,6 +264,7 @@ int fc_topk_encode(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_
     FC_LAUNCHED("k_sample1");
     hipLaunchKernelGGL((k_sample<kKeyMag, 2>), dim3(sgrid), dim3(kBlock), 0, s, g, P, seed, offset, ca.W, ca.ib, hdr, hi);
     FC_LAUNCHED("k_sample2");
+  }
   }
   rc = launch_compact_key(key_mode, ca, s);
   if (rc) return rc;
@@ -243,6 +304,7 @@ int fc_mask_encode(const float* g, uint64_t n, int codec, const uint32_t* mask_b
   a.dir = dir; a.hdr = hdr; a.W = ws_ptrs(ws, n); a.HI = hi;
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid(a.nchunks), blk(kBlock);
+  TimedLaunch t(FC_TIME_COMPACT, s);
   if (mask_bits) {
     if (format == FC_FMT_BITMAP) hipLaunchKernelGGL((k_compact<kKeyMag, kPredMask, FC_FMT_BITMAP>), grid, blk, 0, s, a);
     else hipLaunchKernelGGL((k_compact<kKeyMag, kPredMask, FC_FMT_IDXVAL>), grid, blk, 0, s, a);
@@ -268,6 +330,7 @@ int fc_decode_dense(const fc_packet_view* pkt, int format, uint64_t n, void* out
   a.views = nullptr; a.one = *pkt; a.m = 1; a.n = n; a.out = out;
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid((uint32_t)fc_num_chunks(n)), blk(kBlock);
+  TimedLaunch t(FC_TIME_DECODE, s);
   if (format == FC_FMT_IDXVAL) {
     if (out_f64) hipLaunchKernelGGL((k_decode<FC_FMT_IDXVAL, false, true>), grid, blk, 0, s, a);
     else hipLaunchKernelGGL((k_decode<FC_FMT_IDXVAL, false, false>), grid, blk, 0, s, a);
@@ -291,6 +354,7 @@ int fc_decode_accumulate(const fc_packet_view* views_dev, int m, int format, uin
   a.views = views_dev; a.m = m; a.n = n; a.out = acc;
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid((uint32_t)fc_num_chunks(n)), blk(kBlock);
+  TimedLaunch t(FC_TIME_DECODE, s);
   if (format == FC_FMT_IDXVAL) hipLaunchKernelGGL((k_decode<FC_FMT_IDXVAL, true, false>), grid, blk, 0, s, a);
   else hipLaunchKernelGGL((k_decode<FC_FMT_BITMAP, true, false>), grid, blk, 0, s, a);
   FC_LAUNCHED("k_decode(acc)");

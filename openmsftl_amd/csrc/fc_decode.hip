@@ -185,7 +185,16 @@ __global__ __launch_bounds__(kBlock) void k_wsum(const float* const* rows, const
     const uint64_t e = q * 4;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int r = 0; r < m; ++r) {
-      const float4 x = load4(rows[r], e, n);
+      const float* row = rows[r];
+      float4 x;
+      if (((uintptr_t)row & 15) == 0) {        // rows of an (M, N) G with N % 4 != 0 are not
+        x = load4(row, e, n);                   // 16-B aligned: wave-uniform scalar fallback
+      } else {
+        x.x = e + 0 < n ? row[e + 0] : 0.f;
+        x.y = e + 1 < n ? row[e + 1] : 0.f;
+        x.z = e + 2 < n ? row[e + 2] : 0.f;
+        x.w = e + 3 < n ? row[e + 3] : 0.f;
+      }
       const float wr = w[r];
       const float4 cw = make_float4(__fmul_rn(x.x, wr), __fmul_rn(x.y, wr),
                                     __fmul_rn(x.z, wr), __fmul_rn(x.w, wr));

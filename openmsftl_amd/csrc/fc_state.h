@@ -22,6 +22,7 @@ struct alignas(16) TopkState {
   uint32_t t_lo, t_hi;   // bracket (keys): list key >= t_lo; definite key > t_hi
   uint32_t cand_on, n_hi, n_cand, cand_over, ent_over;
   uint32_t e_shift, e_rank, e_matched, e_done, e_src, e_ticket, e_small_n, e_status;
+  uint32_t dbg[8];
 };
 static_assert(sizeof(TopkState) <= 256, "state block");
 

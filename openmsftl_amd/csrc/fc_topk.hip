@@ -387,32 +387,37 @@ struct EngState {
 
 __device__ __forceinline__ int clz64(uint64_t x) { return x ? __clzll((long long)x) : 64; }
 
+// Every field is assigned on every path (a partially initialised state let hipcc fold the
+// rank of the cand_over path into an undefined register — see DESIGN.md §Lessons).
 template <int KM>
-__device__ __forceinline__ void engine_init(const EngineArgs& a, EngState& E) {
+__device__ __forceinline__ EngState engine_init(const EngineArgs& a) {
   TopkState* S = a.W.st;
   const uint32_t top = 31 + a.ib;          // comps < 2^(31+IB)
-  E.status = FC_STATUS_OK; E.done = 0; E.result = 0;
+  const uint32_t k32 = (uint32_t)a.k;
   if (a.exact) {
-    E.src = 2; E.prefix = 0; E.shift = top; E.rank = (uint32_t)a.k; E.matched = (uint32_t)a.n;
-    if (a.k == 0) { E.done = 1; E.result = kSelectNothing; }
-    else if (a.k >= a.n) { E.done = 1; E.result = 0; }
-    return;
+    const uint32_t done = (a.k == 0 || a.k >= a.n) ? 1u : 0u;
+    const uint64_t res = a.k == 0 ? kSelectNothing : 0ull;
+    return EngState{0ull, top, k32, (uint32_t)a.n, done, 2u, (uint32_t)FC_STATUS_OK, res};
   }
   const uint32_t n_hi = S->n_hi, n_cand = S->n_cand, t_lo = S->t_lo, t_hi = S->t_hi;
   const uint32_t n_ent = a.hdr->n_entries;
-  if (S->ent_over || S->err) { E.done = 1; E.status = FC_STATUS_RETRY_EXACT; return; }
-  if (a.k == 0) { E.done = 1; E.result = kSelectNothing; return; }
-  if ((uint64_t)n_hi + n_cand < a.k) { E.done = 1; E.status = FC_STATUS_RETRY_EXACT; return; }
-  if (n_hi > a.k || S->cand_over) {      // use the listed entries (a superset) instead
-    E.src = 1; E.prefix = 0; E.shift = top; E.rank = (uint32_t)a.k; E.matched = n_ent;
-    return;
-  }
-  E.src = 0; E.rank = (uint32_t)(a.k - n_hi); E.matched = n_cand;
-  if (E.rank == 0) { E.done = 1; E.result = ((uint64_t)t_hi + 1) << a.ib; return; }
+  const bool retry = S->ent_over != 0 || S->err != 0 || (uint64_t)n_hi + n_cand < a.k;
+  if (a.k == 0)
+    return EngState{0ull, top, 0u, 0u, 1u, 2u, (uint32_t)FC_STATUS_OK, kSelectNothing};
+  if (retry)
+    return EngState{0ull, top, k32, 0u, 1u, 2u, (uint32_t)FC_STATUS_RETRY_EXACT, 0ull};
+  const bool use_entries = n_hi > a.k || S->cand_over != 0;   // the listed superset
+  if (use_entries)
+    return EngState{0ull, top, k32, n_ent, 0u, 1u, (uint32_t)FC_STATUS_OK, 0ull};
+  const uint32_t rank = k32 - n_hi;
+  if (rank == 0)
+    return EngState{0ull, top, 0u, n_cand, 1u, 0u, (uint32_t)FC_STATUS_OK,
+                    ((uint64_t)t_hi + 1) << a.ib};
   const uint64_t lo = (uint64_t)t_lo << a.ib;
   const uint64_t hi = ((uint64_t)t_hi << a.ib) | ((1ull << a.ib) - 1);
   const uint32_t sh = 64 - clz64(lo ^ hi);
-  E.shift = sh; E.prefix = sh >= 64 ? 0 : (lo >> sh) << sh;
+  const uint64_t prefix = sh >= 64 ? 0ull : (lo >> sh) << sh;
+  return EngState{prefix, sh, rank, n_cand, 0u, 0u, (uint32_t)FC_STATUS_OK, 0ull};
 }
 
 template <int KM>
@@ -431,14 +436,10 @@ __global__ __launch_bounds__(kBlock) void k_engine(EngineArgs a) {
   __shared__ uint32_t s_tmp[8], s_out[4], s_flag, s_cnt, s_base;
   TopkState* S = a.W.st;
   const int tid = threadIdx.x;
-  EngState E;
-  if (a.first) {
-    engine_init<KM>(a, E);
-  } else {
-    E.prefix = S->e_prefix; E.shift = S->e_shift; E.rank = S->e_rank;
-    E.matched = S->e_matched; E.done = S->e_done; E.src = S->e_src; E.status = S->e_status;
-    E.result = E.prefix;
-  }
+  const EngState E0 = a.first ? engine_init<KM>(a)
+                              : EngState{S->e_prefix, S->e_shift, S->e_rank, S->e_matched,
+                                         S->e_done, S->e_src, S->e_status, S->e_prefix};
+  EngState E = E0;
   if (!a.first && E.done) return;             // resolved by an earlier pass
 
   uint64_t cnt = E.src == 0 ? (uint64_t)min(S->n_cand, (uint32_t)a.W.cand_cap)
