@@ -116,9 +116,8 @@ def main():
     log(f"[rank {rank}] generated {M} x {n:,} fp32 in {time.perf_counter() - t_gen:.1f} s")
 
     lib = L.load()
-    cap = int(lib.fc_topk_capacity(n, k))
     hdrs = torch.empty((M, L.HDR_BYTES), dtype=torch.uint8, device=device)
-    pkts = [codec.Packet.alloc(n, L.FC_FMT_IDXVAL, cap, device, hdr=hdrs[i], k=k)
+    pkts = [codec.Packet.alloc(n, L.FC_FMT_IDXVAL, device, hdr=hdrs[i], k=k)
             for i in range(M)]
     w = [1.0 / (M * world)] * M                 # global FedAVG weights fl32(1/#clients)
     views = codec.views_tensor(pkts, w, device)

@@ -60,7 +60,12 @@ typedef void* fc_stream_t; /* hipStream_t */
 #define FC_FMT_IDXVAL 0      /* uint32 idx[] ascending + float val[] */
 #define FC_FMT_BITMAP 1      /* uint32 bitmap[ceil(N/8192)*256] + float val[] */
 
-#define FC_CHUNK 8192        /* elements per chunk (directory granularity) */
+/* Slotted packet layout: the gradient is cut into chunks of FC_CHUNK elements; chunk c's
+ * entries (ascending index order) live at [c*FC_CHUNK, c*FC_CHUNK + cnt[c]) of idx/val (and
+ * its bitmap words at [c*256, c*256+256)).  Every chunk is encoded by an independent
+ * workgroup — no global scan — so buffers are sized fc_packet_capacity(n) entries while only
+ * the listed entries are written or read. */
+#define FC_CHUNK 8192        /* elements per chunk */
 
 /* Device-resident packet header (96 bytes). */
 typedef struct fc_packet_hdr {
@@ -68,7 +73,7 @@ typedef struct fc_packet_hdr {
   uint64_t lower;       /* L64: every element with comp >= lower is listed             */
   uint32_t n;           /* gradient length                                             */
   uint32_t k;           /* coordinates kept by the codec (top/rand)                    */
-  uint32_t n_entries;   /* entries written to idx/val (>= k: sampled-bracket slack)    */
+  uint32_t n_entries;   /* entries listed (sum of cnt; >= k: sampled-bracket slack)    */
   uint32_t index_bits;  /* IB = max(1, ceil(log2 n))                                   */
   uint32_t codec;       /* FC_CODEC_*                                                  */
   uint32_t status;      /* FC_STATUS_*                                                 */
@@ -88,7 +93,7 @@ typedef struct fc_packet_view {
   const uint32_t* idx;          /* FC_FMT_IDXVAL                        */
   const float* val;
   const uint32_t* bitmap;       /* FC_FMT_BITMAP                        */
-  const uint32_t* dir;          /* ceil(N/FC_CHUNK)+1 entry offsets     */
+  const uint32_t* cnt;          /* ceil(N/FC_CHUNK) entries per chunk   */
   const fc_packet_hdr* hdr;
   float weight;                 /* FedAVG weight w_i (gar.py:37-44)     */
   uint32_t reserved;
@@ -100,24 +105,25 @@ const char* fc_last_error(void);
 /* ---- sizes ------------------------------------------------------------------------- */
 uint64_t fc_num_chunks(uint64_t n);
 size_t fc_workspace_bytes(uint64_t n);        /* scratch for one encoder (one stream)   */
-uint64_t fc_topk_capacity(uint64_t n, uint64_t k); /* idx/val entries a top packet needs */
+uint64_t fc_packet_capacity(uint64_t n);      /* idx/val entries: ceil(n/FC_CHUNK)*FC_CHUNK */
 /* zero a freshly allocated workspace once (self-cleaning afterwards) */
 int fc_workspace_init(void* ws, size_t ws_bytes, fc_stream_t stream);
 
 /* ---- encode: top-k / native rand-k (compression.py:31-45) ---------------------------
  * Single streaming read of g: a sampled bracket [t_lo, t_hi] is estimated from a
- * stratified sample, every element with key >= t_lo is compacted in index order (decoupled
- * look-back, one launch), then the exact k-th composite key is resolved from the bracket's
- * candidates.  hdr->status == FC_STATUS_RETRY_EXACT means the bracket missed (adversarial
- * data): call fc_topk_encode_exact with the same arguments. */
+ * stratified sample, every element with key >= t_lo is compacted in index order into its
+ * chunk's slot (one launch, independent workgroups), then the exact k-th composite key is
+ * resolved from the bracket's candidates.  hdr->status == FC_STATUS_RETRY_EXACT means the
+ * bracket missed (adversarial / tie-heavy data): call fc_topk_encode_exact with the same
+ * arguments.  capacity >= fc_packet_capacity(n); cnt has fc_num_chunks(n) words. */
 int fc_topk_encode(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_t seed,
                    uint64_t offset, uint32_t* idx, float* val, uint64_t capacity,
-                   uint32_t* dir, fc_packet_hdr* hdr, void* ws, size_t ws_bytes,
+                   uint32_t* cnt, fc_packet_hdr* hdr, void* ws, size_t ws_bytes,
                    fc_stream_t stream);
 /* Exact radix-select path (several reads of g); always succeeds; n_entries == k. */
 int fc_topk_encode_exact(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_t seed,
                          uint64_t offset, uint32_t* idx, float* val, uint64_t capacity,
-                         uint32_t* dir, fc_packet_hdr* hdr, void* ws, size_t ws_bytes,
+                         uint32_t* cnt, fc_packet_hdr* hdr, void* ws, size_t ws_bytes,
                          fc_stream_t stream);
 
 /* ---- encode: mask codecs (compression.py:39-60) -------------------------------------
@@ -127,7 +133,7 @@ int fc_topk_encode_exact(const float* g, uint64_t n, uint64_t k, int key_mode, u
  * format: FC_FMT_BITMAP (bitmap required) or FC_FMT_IDXVAL (idx required). */
 int fc_mask_encode(const float* g, uint64_t n, int codec, const uint32_t* mask_bits,
                    double p, uint64_t seed, uint64_t offset, int format, uint32_t* idx,
-                   float* val, uint32_t* bitmap, uint64_t capacity, uint32_t* dir,
+                   float* val, uint32_t* bitmap, uint64_t capacity, uint32_t* cnt,
                    fc_packet_hdr* hdr, void* ws, size_t ws_bytes, fc_stream_t stream);
 
 /* ---- decode (compression.py dense result) --------------------------------------------

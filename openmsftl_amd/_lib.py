@@ -44,7 +44,7 @@ class PacketHdr(ctypes.Structure):
 
 class PacketView(ctypes.Structure):
     _fields_ = [("idx", ctypes.c_void_p), ("val", ctypes.c_void_p),
-                ("bitmap", ctypes.c_void_p), ("dir", ctypes.c_void_p),
+                ("bitmap", ctypes.c_void_p), ("cnt", ctypes.c_void_p),
                 ("hdr", ctypes.c_void_p), ("weight", ctypes.c_float),
                 ("reserved", ctypes.c_uint32)]
 
@@ -61,7 +61,7 @@ SIGNATURES = {
     "fc_last_error": (ctypes.c_char_p, []),
     "fc_num_chunks": (_u64, [_u64]),
     "fc_workspace_bytes": (_sz, [_u64]),
-    "fc_topk_capacity": (_u64, [_u64, _u64]),
+    "fc_packet_capacity": (_u64, [_u64]),
     "fc_workspace_init": (_i32, [_vp, _sz, _vp]),
     "fc_topk_encode": (_i32, [_vp, _u64, _u64, _i32, _u64, _u64, _vp, _vp, _u64, _vp, _vp,
                               _vp, _sz, _vp]),

@@ -6,8 +6,9 @@
     q   = decode(pkt)                      # the dense vector compress() returns
     agg = decode_accumulate(pkts, w)       # aggregation.py:61-63 + gar.py:44, bit-exact fp32
 
-Packets live on the GPU: ``idx``/``val`` (or ``bitmap``/``val``), a per-8192-element chunk
-directory ``dir`` and a 96-byte device header (include/fedcodec.h ``fc_packet_hdr``).
+Packets live on the GPU in the slotted layout of include/fedcodec.h: chunk c (8192 elements)
+lists its entries, ascending, at ``[c*8192, c*8192 + cnt[c])`` of ``idx``/``val`` (or
+``bitmap``/``val``); plus a 96-byte device header (``fc_packet_hdr``).
 """
 from __future__ import annotations
 
@@ -73,21 +74,21 @@ class Packet:
     n: int
     fmt: int
     val: torch.Tensor
-    dir: torch.Tensor
+    cnt: torch.Tensor                      # int32[num_chunks]: entries per chunk slot
     hdr: torch.Tensor                      # uint8[96] (may be a row of a batch tensor)
     idx: Optional[torch.Tensor] = None
     bitmap: Optional[torch.Tensor] = None
     k: int = 0
 
     @classmethod
-    def alloc(cls, n: int, fmt: int, capacity: int, device, hdr: Optional[torch.Tensor] = None,
+    def alloc(cls, n: int, fmt: int, device, hdr: Optional[torch.Tensor] = None,
               k: int = 0) -> "Packet":
         lib = L.load()
         nch = int(lib.fc_num_chunks(n))
-        cap = max(int(capacity), 4)
+        cap = int(lib.fc_packet_capacity(n))
         return cls(n=n, fmt=fmt, k=k,
                    val=torch.empty(cap, dtype=torch.float32, device=device),
-                   dir=torch.empty(nch + 1, dtype=_U32, device=device),
+                   cnt=torch.empty(nch, dtype=_U32, device=device),
                    hdr=hdr if hdr is not None else torch.empty(L.HDR_BYTES, dtype=torch.uint8,
                                                                device=device),
                    idx=torch.empty(cap, dtype=_U32, device=device) if fmt == L.FC_FMT_IDXVAL else None,
@@ -102,7 +103,7 @@ class Packet:
         return L.PacketView(idx=self.idx.data_ptr() if self.idx is not None else 0,
                             val=self.val.data_ptr(),
                             bitmap=self.bitmap.data_ptr() if self.bitmap is not None else 0,
-                            dir=self.dir.data_ptr(), hdr=self.hdr.data_ptr(),
+                            cnt=self.cnt.data_ptr(), hdr=self.hdr.data_ptr(),
                             weight=float(np.float32(weight)), reserved=0)
 
     def header(self) -> L.PacketHdr:
@@ -114,10 +115,12 @@ class Packet:
         """(idx uint32, val float32, header) of every LISTED entry, ascending — includes the
         sampled-bracket slack (comp < thresh); inspection / test helper (synchronises)."""
         h = self.header()
-        ne = h.n_entries
-        val = self.val[:ne].cpu().numpy()
+        cnt = self.cnt.cpu().numpy().astype(np.int64)
+        pos = np.arange(self.capacity, dtype=np.int64)
+        listed = (pos % L.FC_CHUNK) < cnt[pos // L.FC_CHUNK]
+        val = self.val.cpu().numpy()[listed]
         if self.fmt == L.FC_FMT_IDXVAL:
-            idx = self.idx[:ne].cpu().numpy().view(np.uint32)
+            idx = self.idx.cpu().numpy().view(np.uint32)[listed]
         else:
             bits = np.unpackbits(self.bitmap.cpu().numpy().view(np.uint8), bitorder="little")
             idx = np.nonzero(bits[: self.n])[0].astype(np.uint32)
@@ -145,12 +148,11 @@ def encode_top(g: torch.Tensor, k: int, *, key_mode: int = L.FC_KEY_MAGNITUDE, s
         raise ValueError(f"k={k} outside [0, {n}]")
     ws = Workspace.get(n, g.device)
     if packet is None:
-        cap = int(lib.fc_topk_capacity(n, k))
-        packet = Packet.alloc(n, L.FC_FMT_IDXVAL, cap, g.device, k=k)
+        packet = Packet.alloc(n, L.FC_FMT_IDXVAL, g.device, k=k)
     packet.k = k
     fn = lib.fc_topk_encode_exact if exact else lib.fc_topk_encode
     L.check(fn(_vp(g), n, k, key_mode, seed, offset, _vp(packet.idx), _vp(packet.val),
-               packet.capacity, _vp(packet.dir), _vp(packet.hdr), _vp(ws.buf), ws.nbytes,
+               packet.capacity, _vp(packet.cnt), _vp(packet.hdr), _vp(ws.buf), ws.nbytes,
                _stream(g.device)), "fc_topk_encode")
     packet._enc = (g, k, key_mode, seed, offset)
     if check:
@@ -172,7 +174,7 @@ def resolve(packets: Sequence[Packet]) -> int:
         g, k, key_mode, seed, offset = p._enc
         ws = Workspace.get(g.numel(), g.device)
         L.check(lib.fc_topk_encode_exact(_vp(g), g.numel(), k, key_mode, seed, offset,
-                                         _vp(p.idx), _vp(p.val), p.capacity, _vp(p.dir),
+                                         _vp(p.idx), _vp(p.val), p.capacity, _vp(p.cnt),
                                          _vp(p.hdr), _vp(ws.buf), ws.nbytes,
                                          _stream(g.device)), "fc_topk_encode_exact")
         redo += 1
@@ -184,8 +186,7 @@ def resolve(packets: Sequence[Packet]) -> int:
 
 def encode_mask(g: torch.Tensor, codec: int, *, p: float = 0.5,
                 mask_bits: Optional[torch.Tensor] = None, seed: int = 0, offset: int = 0,
-                fmt: int = L.FC_FMT_BITMAP, packet: Optional[Packet] = None,
-                capacity: Optional[int] = None) -> Packet:
+                fmt: int = L.FC_FMT_BITMAP, packet: Optional[Packet] = None) -> Packet:
     """Mask codecs: dropout-biased / dropout-unbiased (Philox or host mask) and rand-k with a
     host-drawn permutation mask (parity mode).  ``mask_bits``: int32 device tensor, bit i of
     word i//32 = element i."""
@@ -197,10 +198,10 @@ def encode_mask(g: torch.Tensor, codec: int, *, p: float = 0.5,
                                   or mask_bits.numel() * 32 < n):
         raise ValueError("mask_bits must be an int32 CUDA tensor of ceil(n/32) words")
     if packet is None:
-        packet = Packet.alloc(n, fmt, capacity if capacity is not None else n, g.device)
+        packet = Packet.alloc(n, fmt, g.device)
     L.check(lib.fc_mask_encode(_vp(g), n, codec, _vp(mask_bits), float(p), seed, offset, fmt,
                                _vp(packet.idx), _vp(packet.val), _vp(packet.bitmap),
-                               packet.capacity, _vp(packet.dir), _vp(packet.hdr), _vp(ws.buf),
+                               packet.capacity, _vp(packet.cnt), _vp(packet.hdr), _vp(ws.buf),
                                ws.nbytes, _stream(g.device)), "fc_mask_encode")
     return packet
 

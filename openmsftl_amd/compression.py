@@ -89,8 +89,7 @@ class Compression:
                 pkt = codec.encode_top(g, k)
             elif host_idx is not None:
                 mask = torch.from_numpy(bitmask_words(host_idx, n, False).view(np.int32)).to(g.device)
-                pkt = codec.encode_mask(g, L.FC_CODEC_RAND, mask_bits=mask, fmt=L.FC_FMT_IDXVAL,
-                                        capacity=max(k, 1))
+                pkt = codec.encode_mask(g, L.FC_CODEC_RAND, mask_bits=mask, fmt=L.FC_FMT_IDXVAL)
             else:
                 pkt = codec.encode_top(g, k, key_mode=L.FC_KEY_PHILOX, seed=self.seed,
                                        offset=self._next_offset())

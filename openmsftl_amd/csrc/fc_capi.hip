@@ -1,9 +1,9 @@
 // fc_capi.hip — extern "C" entry points of libfedcodec.so (declared in include/fedcodec.h).
 // Argument checking, sampling plans and launch sequences; no allocation, no host syncs.
 #include <math.h>
-#include <stdlib.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <vector>
@@ -38,6 +38,8 @@ static uint32_t index_bits(uint64_t n) {
   return b;
 }
 
+static uint32_t num_chunks(uint64_t n) { return (uint32_t)((n + kChunk - 1) / kChunk); }
+
 static WsPtrs ws_ptrs(void* ws, uint64_t n) {
   const WsLayout L = WsLayout::of(n);
   char* b = static_cast<char*>(ws);
@@ -47,8 +49,9 @@ static WsPtrs ws_ptrs(void* ws, uint64_t n) {
   W.hist2h = reinterpret_cast<uint32_t*>(b + L.off_hist2h);
   W.hist2l = reinterpret_cast<uint32_t*>(b + L.off_hist2l);
   W.ehist = reinterpret_cast<uint32_t*>(b + L.off_ehist);
+  W.chist = reinterpret_cast<uint32_t*>(b + L.off_chist);
   W.small = reinterpret_cast<uint64_t*>(b + L.off_small);
-  W.status = reinterpret_cast<uint64_t*>(b + L.off_status);
+  W.ccnt = reinterpret_cast<uint32_t*>(b + L.off_status);
   W.cand = reinterpret_cast<uint64_t*>(b + L.off_cand);
   W.cand_cap = L.cand_cap;
   return W;
@@ -75,7 +78,6 @@ static SamplePlan make_plan(uint64_t n, uint64_t k) {
     const double m = 6.0 * sqrt(S * q * (1.0 - q)) + 16.0;
     P.r_hi = (int64_t)floor(rho - m);
     P.r_lo = (int64_t)ceil(rho + m);
-    if (P.r_hi < 1) P.hi_none = 1;
     if (P.r_lo > (int64_t)S) P.lo_all = 1;
   }
   if (P.r_hi < 1) P.hi_none = 1;
@@ -142,26 +144,21 @@ static int launch_compact_key(int key_mode, const CompactArgs& a, hipStream_t s)
   return FC_OK;
 }
 
+static int launch_resolve(const ResolveArgs& a, hipStream_t s) {
+  TimedLaunch t(FC_TIME_ENGINE, s);
+  const uint32_t grid = a.nchunks < (uint32_t)kResolveGrid ? a.nchunks : (uint32_t)kResolveGrid;
+  hipLaunchKernelGGL(k_resolve, dim3(grid), dim3(kBlock), 0, s, a);
+  FC_LAUNCHED("k_resolve");
+  return FC_OK;
+}
+
 extern "C" {
 
 int fc_abi_version(void) { return FC_ABI_VERSION; }
 const char* fc_last_error(void) { return g_err; }
-uint64_t fc_num_chunks(uint64_t n) { return (n + kChunk - 1) / kChunk; }
+uint64_t fc_num_chunks(uint64_t n) { return num_chunks(n); }
 size_t fc_workspace_bytes(uint64_t n) { return (size_t)WsLayout::of(n).bytes; }
-
-uint64_t fc_topk_capacity(uint64_t n, uint64_t k) {
-  // k plus the bracket slack: 6 sigma of the sample quantile on each side, scaled to n,
-  // plus a floor; the encoder reports FC_STATUS_OVERFLOW (never corrupts) beyond this.
-  if (n <= kFullSampleMax) return n;
-  const double q = (double)k / (double)n;
-  uint64_t seg = n / 32 / 1024;
-  if (seg < 64) seg = 64;
-  if (seg > 1024) seg = 1024;
-  const double S = (double)seg * 1024.0;
-  const double slack = (2.0 * (6.0 * sqrt(S * q * (1.0 - q)) + 16.0) + 2048.0) / S * (double)n;
-  uint64_t cap = k + (uint64_t)(1.5 * slack) + 65536;
-  return cap > n ? n : cap;
-}
+uint64_t fc_packet_capacity(uint64_t n) { return (uint64_t)num_chunks(n) * kChunk; }
 
 int fc_timing_begin(uint32_t mask) {
   g_time_mask = mask;
@@ -198,41 +195,44 @@ int fc_workspace_init(void* ws, size_t ws_bytes, fc_stream_t stream) {
 
 static int topk_args(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_t seed,
                      uint64_t offset, uint32_t* idx, float* val, uint64_t capacity,
-                     uint32_t* dir, fc_packet_hdr* hdr, void* ws, size_t ws_bytes,
-                     CompactArgs* ca, EngineArgs* ea, HdrInit* hi) {
+                     uint32_t* cnt, fc_packet_hdr* hdr, void* ws, size_t ws_bytes,
+                     CompactArgs* ca, EngineArgs* ea, ResolveArgs* ra, HdrInit* hi) {
   int rc = check_common(g, n, ws, ws_bytes);
   if (rc) return rc;
-  FC_CHECK(idx && val && dir && hdr, "packet buffers must be non-NULL");
+  FC_CHECK(idx && val && cnt && hdr, "packet buffers must be non-NULL");
   FC_CHECK(key_mode == FC_KEY_MAGNITUDE || key_mode == FC_KEY_PHILOX, "bad key_mode %d", key_mode);
   FC_CHECK(k <= n, "k=%llu > n=%llu (pass the effective k)", (unsigned long long)k,
            (unsigned long long)n);
-  FC_CHECK(capacity >= k, "capacity %llu < k %llu", (unsigned long long)capacity,
-           (unsigned long long)k);
+  FC_CHECK(capacity >= fc_packet_capacity(n), "capacity %llu < fc_packet_capacity(n) %llu",
+           (unsigned long long)capacity, (unsigned long long)fc_packet_capacity(n));
   const uint32_t ib = index_bits(n);
   memset(hi, 0, sizeof *hi);
   hi->seed = seed; hi->offset = offset; hi->p = 0.0; hi->n = (uint32_t)n; hi->k = (uint32_t)k;
   hi->ib = ib; hi->codec = key_mode == FC_KEY_PHILOX ? FC_CODEC_RAND : FC_CODEC_TOP;
   hi->format = FC_FMT_IDXVAL; hi->key_mode = (uint32_t)key_mode;
   memset(ca, 0, sizeof *ca);
-  ca->g = g; ca->n = n; ca->ib = ib; ca->nchunks = (uint32_t)fc_num_chunks(n);
-  ca->seed = seed; ca->offset = offset; ca->idx = idx; ca->val = val; ca->cap = capacity;
-  ca->dir = dir; ca->hdr = hdr; ca->W = ws_ptrs(ws, n); ca->HI = *hi;
+  ca->g = g; ca->n = n; ca->ib = ib; ca->nchunks = num_chunks(n);
+  ca->seed = seed; ca->offset = offset; ca->idx = idx; ca->val = val; ca->cnt = cnt;
+  ca->hdr = hdr; ca->W = ws_ptrs(ws, n); ca->HI = *hi;
   memset(ea, 0, sizeof *ea);
-  ea->g = g; ea->n = n; ea->idx = idx; ea->val = val; ea->ib = ib; ea->k = k;
+  ea->g = g; ea->n = n; ea->ib = ib; ea->k = k;
   ea->seed = seed; ea->offset = offset; ea->hdr = hdr; ea->W = ca->W; ea->HI = *hi;
+  memset(ra, 0, sizeof *ra);
+  ra->ib = ib; ra->nchunks = ca->nchunks; ra->k = k; ra->idx = idx; ra->val = val; ra->cnt = cnt;
+  ra->seed = seed; ra->offset = offset; ra->key_mode = (uint32_t)key_mode;
+  ra->hdr = hdr; ra->W = ca->W;
   return FC_OK;
 }
 
 int fc_topk_encode_exact(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_t seed,
                          uint64_t offset, uint32_t* idx, float* val, uint64_t capacity,
-                         uint32_t* dir, fc_packet_hdr* hdr, void* ws, size_t ws_bytes,
+                         uint32_t* cnt, fc_packet_hdr* hdr, void* ws, size_t ws_bytes,
                          fc_stream_t stream) {
-  CompactArgs ca; EngineArgs ea; HdrInit hi;
-  int rc = topk_args(g, n, k, key_mode, seed, offset, idx, val, capacity, dir, hdr, ws,
-                     ws_bytes, &ca, &ea, &hi);
+  CompactArgs ca; EngineArgs ea; ResolveArgs ra; HdrInit hi;
+  int rc = topk_args(g, n, k, key_mode, seed, offset, idx, val, capacity, cnt, hdr, ws,
+                     ws_bytes, &ca, &ea, &ra, &hi);
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
-  ea.exact = 1;
   rc = launch_engine(key_mode, ea, kEnginePasses, s);
   if (rc) return rc;
   return launch_compact_key(key_mode, ca, s);
@@ -240,50 +240,51 @@ int fc_topk_encode_exact(const float* g, uint64_t n, uint64_t k, int key_mode, u
 
 int fc_topk_encode(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_t seed,
                    uint64_t offset, uint32_t* idx, float* val, uint64_t capacity,
-                   uint32_t* dir, fc_packet_hdr* hdr, void* ws, size_t ws_bytes,
+                   uint32_t* cnt, fc_packet_hdr* hdr, void* ws, size_t ws_bytes,
                    fc_stream_t stream) {
   if (k == 0 || k >= n)  // trivial thresholds: the exact engine resolves them in its init
-    return fc_topk_encode_exact(g, n, k, key_mode, seed, offset, idx, val, capacity, dir, hdr,
+    return fc_topk_encode_exact(g, n, k, key_mode, seed, offset, idx, val, capacity, cnt, hdr,
                                 ws, ws_bytes, stream);
-  CompactArgs ca; EngineArgs ea; HdrInit hi;
-  int rc = topk_args(g, n, k, key_mode, seed, offset, idx, val, capacity, dir, hdr, ws,
-                     ws_bytes, &ca, &ea, &hi);
+  CompactArgs ca; EngineArgs ea; ResolveArgs ra; HdrInit hi;
+  int rc = topk_args(g, n, k, key_mode, seed, offset, idx, val, capacity, cnt, hdr, ws,
+                     ws_bytes, &ca, &ea, &ra, &hi);
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
   const SamplePlan P = make_plan(n, k);
-  const uint32_t sgrid = P.nseg < 1024 ? P.nseg : 1024;
+  const uint32_t sgrid = P.nseg < 256 ? P.nseg : 256;
   {
-  TimedLaunch t(FC_TIME_SAMPLE, s);
-  if (key_mode == FC_KEY_PHILOX) {
-    hipLaunchKernelGGL((k_sample<kKeyPhilox, 1>), dim3(sgrid), dim3(kBlock), 0, s, g, P, seed, offset, ca.W, ca.ib, hdr, hi);
-    FC_LAUNCHED("k_sample1");
-    hipLaunchKernelGGL((k_sample<kKeyPhilox, 2>), dim3(sgrid), dim3(kBlock), 0, s, g, P, seed, offset, ca.W, ca.ib, hdr, hi);
-    FC_LAUNCHED("k_sample2");
-  } else {
-    hipLaunchKernelGGL((k_sample<kKeyMag, 1>), dim3(sgrid), dim3(kBlock), 0, s, g, P, seed, offset, ca.W, ca.ib, hdr, hi);
-    FC_LAUNCHED("k_sample1");
-    hipLaunchKernelGGL((k_sample<kKeyMag, 2>), dim3(sgrid), dim3(kBlock), 0, s, g, P, seed, offset, ca.W, ca.ib, hdr, hi);
-    FC_LAUNCHED("k_sample2");
-  }
+    TimedLaunch t(FC_TIME_SAMPLE, s);
+    if (key_mode == FC_KEY_PHILOX) {
+      hipLaunchKernelGGL((k_sample<kKeyPhilox, 1>), dim3(sgrid), dim3(kBlock), 0, s, g, P, seed, offset, ca.W, ca.ib, hdr, hi);
+      FC_LAUNCHED("k_sample1");
+      hipLaunchKernelGGL((k_sample<kKeyPhilox, 2>), dim3(sgrid), dim3(kBlock), 0, s, g, P, seed, offset, ca.W, ca.ib, hdr, hi);
+      FC_LAUNCHED("k_sample2");
+    } else {
+      hipLaunchKernelGGL((k_sample<kKeyMag, 1>), dim3(sgrid), dim3(kBlock), 0, s, g, P, seed, offset, ca.W, ca.ib, hdr, hi);
+      FC_LAUNCHED("k_sample1");
+      hipLaunchKernelGGL((k_sample<kKeyMag, 2>), dim3(sgrid), dim3(kBlock), 0, s, g, P, seed, offset, ca.W, ca.ib, hdr, hi);
+      FC_LAUNCHED("k_sample2");
+    }
   }
   rc = launch_compact_key(key_mode, ca, s);
   if (rc) return rc;
-  ea.exact = 0;
-  return launch_engine(key_mode, ea, kEnginePasses, s);
+  return launch_resolve(ra, s);
 }
 
 int fc_mask_encode(const float* g, uint64_t n, int codec, const uint32_t* mask_bits, double p,
                    uint64_t seed, uint64_t offset, int format, uint32_t* idx, float* val,
-                   uint32_t* bitmap, uint64_t capacity, uint32_t* dir, fc_packet_hdr* hdr,
+                   uint32_t* bitmap, uint64_t capacity, uint32_t* cnt, fc_packet_hdr* hdr,
                    void* ws, size_t ws_bytes, fc_stream_t stream) {
   int rc = check_common(g, n, ws, ws_bytes);
   if (rc) return rc;
   FC_CHECK(codec == FC_CODEC_DROPOUT_BIASED || codec == FC_CODEC_DROPOUT_UNBIASED ||
                codec == FC_CODEC_RAND, "bad codec %d", codec);
   FC_CHECK(format == FC_FMT_IDXVAL || format == FC_FMT_BITMAP, "bad format %d", format);
-  FC_CHECK(val && dir && hdr, "packet buffers must be non-NULL");
+  FC_CHECK(val && cnt && hdr, "packet buffers must be non-NULL");
   FC_CHECK(format != FC_FMT_IDXVAL || idx, "idx required for FC_FMT_IDXVAL");
   FC_CHECK(format != FC_FMT_BITMAP || bitmap, "bitmap required for FC_FMT_BITMAP");
+  FC_CHECK(capacity >= fc_packet_capacity(n), "capacity %llu < fc_packet_capacity(n) %llu",
+           (unsigned long long)capacity, (unsigned long long)fc_packet_capacity(n));
   FC_CHECK(mask_bits || (p >= 0.0 && p <= 1.0), "p=%g outside [0, 1]", p);
   FC_CHECK(mask_bits || codec != FC_CODEC_RAND, "native rand-k uses fc_topk_encode(PHILOX)");
   HdrInit hi;
@@ -293,15 +294,15 @@ int fc_mask_encode(const float* g, uint64_t n, int codec, const uint32_t* mask_b
   hi.key_mode = FC_KEY_MAGNITUDE;
   CompactArgs a;
   memset(&a, 0, sizeof a);
-  a.g = g; a.n = n; a.ib = hi.ib; a.nchunks = (uint32_t)fc_num_chunks(n);
+  a.g = g; a.n = n; a.ib = hi.ib; a.nchunks = num_chunks(n);
   a.seed = seed; a.offset = offset; a.mask = mask_bits;
   double thr = floor(p * 4294967296.0 + 0.5);
   if (thr < 0) thr = 0;
   if (thr > 4294967296.0) thr = 4294967296.0;
   a.bern_thr = (uint64_t)thr;
   a.nonfinite_keep = codec != FC_CODEC_RAND;
-  a.write_hdr = 1; a.idx = idx; a.val = val; a.bitmap = bitmap; a.cap = capacity;
-  a.dir = dir; a.hdr = hdr; a.W = ws_ptrs(ws, n); a.HI = hi;
+  a.write_hdr = 1; a.idx = idx; a.val = val; a.bitmap = bitmap; a.cnt = cnt;
+  a.hdr = hdr; a.W = ws_ptrs(ws, n); a.HI = hi;
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid(a.nchunks), blk(kBlock);
   TimedLaunch t(FC_TIME_COMPACT, s);
@@ -321,7 +322,7 @@ int fc_decode_dense(const fc_packet_view* pkt, int format, uint64_t n, void* out
   FC_CHECK(pkt && out, "NULL argument");
   FC_CHECK(n >= 1 && n <= 0xffffffffull, "bad n");
   FC_CHECK(format == FC_FMT_IDXVAL || format == FC_FMT_BITMAP, "bad format %d", format);
-  FC_CHECK(pkt->dir && pkt->hdr && pkt->val, "packet view incomplete");
+  FC_CHECK(pkt->cnt && pkt->hdr && pkt->val, "packet view incomplete");
   FC_CHECK(format != FC_FMT_IDXVAL || pkt->idx, "idx missing");
   FC_CHECK(format != FC_FMT_BITMAP || pkt->bitmap, "bitmap missing");
   FC_CHECK(((uintptr_t)out & 15) == 0, "out must be 16-byte aligned");
@@ -329,7 +330,7 @@ int fc_decode_dense(const fc_packet_view* pkt, int format, uint64_t n, void* out
   memset(&a, 0, sizeof a);
   a.views = nullptr; a.one = *pkt; a.m = 1; a.n = n; a.out = out;
   hipStream_t s = (hipStream_t)stream;
-  const dim3 grid((uint32_t)fc_num_chunks(n)), blk(kBlock);
+  const dim3 grid(num_chunks(n)), blk(kBlock);
   TimedLaunch t(FC_TIME_DECODE, s);
   if (format == FC_FMT_IDXVAL) {
     if (out_f64) hipLaunchKernelGGL((k_decode<FC_FMT_IDXVAL, false, true>), grid, blk, 0, s, a);
@@ -353,7 +354,7 @@ int fc_decode_accumulate(const fc_packet_view* views_dev, int m, int format, uin
   memset(&a, 0, sizeof a);
   a.views = views_dev; a.m = m; a.n = n; a.out = acc;
   hipStream_t s = (hipStream_t)stream;
-  const dim3 grid((uint32_t)fc_num_chunks(n)), blk(kBlock);
+  const dim3 grid(num_chunks(n)), blk(kBlock);
   TimedLaunch t(FC_TIME_DECODE, s);
   if (format == FC_FMT_IDXVAL) hipLaunchKernelGGL((k_decode<FC_FMT_IDXVAL, true, false>), grid, blk, 0, s, a);
   else hipLaunchKernelGGL((k_decode<FC_FMT_BITMAP, true, false>), grid, blk, 0, s, a);

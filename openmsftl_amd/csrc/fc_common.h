@@ -19,22 +19,16 @@ constexpr int kChunk = kBlock * 4 * kVec;   // 8192 elements
 constexpr int kChunkWords = kChunk / 32;    // bitmap words per chunk (256)
 constexpr int kHistBits = 12;
 constexpr int kHistBins = 1 << kHistBits;   // 4096
-constexpr int kSmallCap = 2048;             // exact-finish list (LDS bitonic)
+constexpr int kSmallCap = 4096;             // exact-finish list (LDS bitonic, 32 KiB)
 constexpr int kEngineGrid = 256;            // radix-engine workgroups (one per CU)
 constexpr int kEnginePasses = 6;            // ceil(63 / 12): enough for any comp width
+constexpr int kResolveGrid = 256;           // k_resolve workgroups
+constexpr int kSlots = kVec * kWaves;       // 32 (i, w) slots per chunk
+constexpr int kCandSlot = 256;              // candidate slot per chunk (overflow: re-read entries)
+constexpr int kShards = 64;                 // sharded k_compact totals
 
 constexpr uint32_t kNanKey = 0x7f800001u;   // every NaN sorts above +inf
 constexpr uint64_t kSelectNothing = 1ull << 63;
-
-// ---- status granules (decoupled look-back) -------------------------------------------
-// [63:34] epoch (30 bits) | [33:32] flag | [31:0] value
-constexpr uint64_t kFlagAgg = 1, kFlagInc = 2;
-__device__ __forceinline__ uint64_t granule(uint32_t epoch, uint64_t flag, uint32_t v) {
-  return ((uint64_t)(epoch & 0x3fffffffu) << 34) | (flag << 32) | v;
-}
-__device__ __forceinline__ uint32_t g_epoch(uint64_t s) { return (uint32_t)(s >> 34); }
-__device__ __forceinline__ uint32_t g_flag(uint64_t s) { return (uint32_t)(s >> 32) & 3u; }
-__device__ __forceinline__ uint32_t g_val(uint64_t s) { return (uint32_t)s; }
 
 template <typename T>
 __device__ __forceinline__ T ld_agent(const T* p) {
@@ -145,6 +139,19 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_tmp,
   __syncthreads();
   if (total) *total = tot;
   return base + inc - v;
+}
+
+// Last-arriver ticket for payloads written ONLY by agent-scope atomics or sc1 stores and
+// read ONLY by sc1 loads / atomics (MI355X_MICROARCH.md §visibility, "Hand-offs measured
+// with sc1 loads": every storing wave drains, barrier, one lane adds; the workgroup whose
+// add returned nblocks-1 loads after a barrier).  No L2 write-back fence needed.
+__device__ __forceinline__ bool last_block_arrive_sc1(uint32_t* counter, uint32_t nblocks,
+                                                      uint32_t* s_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) *s_flag = (atomicAdd(counter, 1u) == nblocks - 1) ? 1u : 0u;
+  __syncthreads();
+  return *s_flag != 0;
 }
 
 // Workgroup "last arriver" ticket (MI355X_MICROARCH.md §visibility valid producer form):

@@ -1,7 +1,7 @@
 // fc_decode.hip — packet decode and bit-exact FedAVG accumulation for MI355X (gfx950).
 //
 // k_decode<FMT, ACC, OutT>: one workgroup per 8192-element chunk.  For each packet (client,
-// in G's row order) the chunk's entries [dir[c], dir[c+1]) are expanded:
+// in G's row order) the chunk's slot entries [c*8192, c*8192 + cnt[c]) are expanded:
 //   FC_FMT_IDXVAL : entries scattered into an LDS tile + LDS presence bitmap (keeps only
 //                   comp >= T64, the sampled-bracket slack is dropped here)
 //   FC_FMT_BITMAP : the chunk's 256 bitmap words are prefix-counted in LDS and every lane
@@ -19,7 +19,7 @@ struct PktCache {
   const uint32_t* idx;
   const float* val;
   const uint32_t* bitmap;
-  const uint32_t* dir;
+  const uint32_t* cnt;
   uint64_t thresh, seed, offset;
   double p;
   uint32_t ib, codec, key_mode;
@@ -28,7 +28,7 @@ struct PktCache {
 
 __device__ __forceinline__ PktCache load_pkt(const fc_packet_view& v) {
   PktCache c;
-  c.idx = v.idx; c.val = v.val; c.bitmap = v.bitmap; c.dir = v.dir; c.w = v.weight;
+  c.idx = v.idx; c.val = v.val; c.bitmap = v.bitmap; c.cnt = v.cnt; c.w = v.weight;
   const fc_packet_hdr* h = v.hdr;
   c.thresh = h->thresh; c.seed = h->seed; c.offset = h->offset; c.p = h->p;
   c.ib = h->index_bits; c.codec = h->codec; c.key_mode = h->key_mode;
@@ -94,7 +94,7 @@ __global__ __launch_bounds__(kBlock) void k_decode(DecodeArgs a) {
 
   for (int m = 0; m < a.m; ++m) {
     const PktCache pk = load_pkt(ACC ? a.views[m] : a.one);
-    const uint32_t lo = pk.dir[c], hi = pk.dir[c + 1];
+    const uint32_t lo = c * (uint32_t)kChunk, hi = lo + pk.cnt[c];   // chunk c's slot
     __syncthreads();                                     // previous packet fully consumed
     if (FMT == FC_FMT_IDXVAL) {
       bits[tid] = 0;

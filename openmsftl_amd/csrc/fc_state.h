@@ -1,4 +1,4 @@
-// fc_state.h — encoder workspace layout + kernel argument blocks (device and host views).
+// fc_state.h — encoder workspace layout + shared argument blocks (device and host views).
 #pragma once
 #include <stdint.h>
 #include "../../include/fedcodec.h"
@@ -7,39 +7,46 @@
 namespace fc {
 
 // Per-encoder state.  Self-cleaning: every counter a kernel consumes is reset by the
-// last-arriving workgroup of the launch that consumed it, so a stream of encodes (or a
-// graph replay) needs the workspace zeroed only once (fc_workspace_init).
+// workgroup that consumed it last, so a stream of encodes (or a graph replay) needs the
+// workspace zeroed only once (fc_workspace_init).
 struct alignas(16) TopkState {
   uint64_t ticket;       // k_compact chunk tickets {epoch:32 | count:32}; the holder of the
                          // last ticket starts the next epoch at count 0
   uint64_t L64;          // entries written: comp >= L64
-  uint64_t e_prefix;     // radix engine: resolved high bits of T64
+  uint64_t e_prefix;     // exact radix engine: resolved high bits of T64
   uint32_t err;          // sticky device error (spin timeout)
-  uint32_t a_done, b_done;
+  uint32_t a_done, b_done, r_done;
   uint32_t b1_hi, b1_lo; // level-1 sample bins of the two bracket ranks
   uint32_t rr_hi, rr_lo; // residual 1-based ranks inside those bins
   uint32_t hi_none, lo_all;
-  uint32_t t_lo, t_hi;   // bracket (keys): list key >= t_lo; definite key > t_hi
-  uint32_t cand_on, n_hi, n_cand, cand_over, ent_over;
-  uint32_t e_shift, e_rank, e_matched, e_done, e_src, e_ticket, e_small_n, e_status;
-  uint32_t dbg[8];
+  uint32_t t_lo, t_hi;   // bracket (keys): list key >= t_lo; candidates key <= t_hi
+  uint32_t sbin;         // candidate histogram bin = (key - t_lo) >> sbin  (< 4096 bins)
+  uint32_t cand_on, n_cand, cand_over, ent_over;
+  uint32_t small_n;      // survivors gathered for the LDS finish
+  uint32_t e_shift, e_rank, e_matched, e_done, e_ticket, e_status;
+  uint32_t pad_[6];
+  uint32_t shard_ent[kShards];   // k_compact totals, 64-way sharded (no hot word)
+  uint32_t shard_cnd[kShards];
 };
-static_assert(sizeof(TopkState) <= 256, "state block");
+static_assert(sizeof(TopkState) <= 1024, "state block");
 
 struct WsLayout {
   uint64_t nchunks, cand_cap;
-  uint64_t off_hist1, off_hist2h, off_hist2l, off_ehist, off_small, off_status, off_cand, bytes;
+  uint64_t off_hist1, off_hist2h, off_hist2l, off_ehist, off_chist, off_small, off_status,
+      off_cand, bytes;
   __host__ __device__ static WsLayout of(uint64_t n) {
     WsLayout L;
     L.nchunks = (n + kChunk - 1) / kChunk;
-    L.cand_cap = n / 32 > 65536 ? n / 32 : 65536;
-    uint64_t o = 256;
+    L.cand_cap = L.nchunks * kCandSlot;                // per-chunk candidate slots
+    uint64_t o = 1024;
     L.off_hist1 = o;  o += 4ull * kHistBins;
     L.off_hist2h = o; o += 4ull * kHistBins;
     L.off_hist2l = o; o += 4ull * kHistBins;
     L.off_ehist = o;  o += 4ull * kHistBins;
+    L.off_chist = o;  o += 4ull * kHistBins;
     L.off_small = o;  o += 8ull * kSmallCap;
-    L.off_status = o; o += 8ull * (L.nchunks ? L.nchunks : 1);
+    L.off_status = o; o += 4ull * (L.nchunks ? L.nchunks : 1);   // per-chunk candidate counts
+    o = (o + 15) & ~15ull;
     L.off_cand = o;   o += 8ull * L.cand_cap;
     L.bytes = (o + 255) & ~255ull;
     return L;
@@ -54,8 +61,10 @@ struct HdrInit {          // static header fields, written by the first kernel o
 
 struct WsPtrs {
   TopkState* st;
-  uint32_t *hist1, *hist2h, *hist2l, *ehist;
-  uint64_t *small, *status, *cand;
+  uint32_t *hist1, *hist2h, *hist2l, *ehist, *chist;
+  uint64_t* small;
+  uint32_t* ccnt;          // candidates per chunk (may exceed kCandSlot: overflowed chunk)
+  uint64_t* cand;          // chunk c's candidates at [c * kCandSlot, + min(ccnt, kCandSlot))
   uint64_t cand_cap;
 };
 

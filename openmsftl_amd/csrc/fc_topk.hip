@@ -1,22 +1,28 @@
 // fc_topk.hip — top-k / native rand-k encode for MI355X (gfx950).
 //
-// Replaces compression.py:31-45 (argsort(|g|)[::-1][:k] / permutation[:k]) with a
-// streaming select whose only full read of g is ONE compaction launch:
+// Replaces compression.py:31-45 (argsort(|g|)[::-1][:k] / permutation[:k]).  Fast path =
+// four launches, ONE streaming read of g:
 //
-//   k_sample_l1, k_sample_l2   stratified sample (<= 1 M keys, <1 % of g) -> two-level
-//                              4096-bin histograms -> bracket [t_lo, t_hi] around the k-th key
-//   k_compact                  one pass over g: every element with key >= t_lo is written
-//                              (idx, val) in ascending index order (decoupled look-back over
-//                              8192-element chunks); keys inside the bracket are also
-//                              appended to a small candidate list; keys above t_hi counted
-//   k_engine (x <= 6)          radix select (12-bit digits, LDS histograms) on the
-//                              candidates -> exact composite threshold T64; finishes with an
-//                              LDS bitonic sort once <= 2048 candidates remain
+//   k_sample<1>, k_sample<2>  stratified sample (<= 1 M keys, < 1 % of g) -> two-level
+//                             4096-bin histograms -> key bracket [t_lo, t_hi] around the
+//                             k-th key (+-6 sigma of the sample quantile)
+//   k_compact                 one pass over g, one independent 256-thread workgroup per
+//                             8192-element chunk: every element with key >= t_lo is written
+//                             (idx, val) in ascending index order into the chunk's SLOT of the
+//                             packet ([c*8192, c*8192 + cnt[c])) — no global scan, no
+//                             look-back; keys inside the bracket ("candidates") also go to the
+//                             chunk's candidate slot and a 4096-bin histogram
+//   k_resolve                 histogram -> the bin holding rank r = k - #(key > t_hi);
+//                             gather that bin's candidates; LDS bitonic sort -> exact T64
 //
-// Selection rule: comp = key << IB | idx is unique per element, the k
+// Anything unusual (bracket missed, candidate list overflow, > 4096 survivors) sets
+// FC_STATUS_RETRY_EXACT; fc_topk_encode_exact then runs k_engine (12-bit radix select over
+// g, <= 6 passes) followed by k_compact with L64 = T64 (no slack).
+//
+// Selection rule: comp = key << IB | idx is unique per element; the k
 // largest comps are kept <=> argsort(|g|, stable)[::-1][:k] (highest index first in a tie),
-// NaN above +inf.  The packet keeps every element with comp >= L64 (L64 <= T64); the decoder
-// keeps comp >= T64.  fc_topk_encode_exact runs the same engine over g itself (no bracket).
+// NaN above +inf.  The packet lists every element with comp >= L64 (L64 <= T64); decoders
+// keep comp >= T64.
 #include "fc_state.h"
 
 namespace fc {
@@ -39,6 +45,7 @@ __device__ __forceinline__ uint32_t u4get(const uint4& v, int j) {
 
 // Find the bin holding the rank1-th largest element (1-based, descending bins) of an LDS
 // histogram of kHistBins counts.  Result in s_out[0] = bin, s_out[1] = 1-based rank inside.
+// Requires a 256-thread workgroup.
 __device__ void find_rank_desc(const uint32_t* h, uint32_t rank1, uint32_t* s_tmp,
                                uint32_t* s_out) {
   const int t = threadIdx.x;
@@ -62,9 +69,24 @@ __device__ void find_rank_desc(const uint32_t* h, uint32_t rank1, uint32_t* s_tm
   __syncthreads();
 }
 
+// Descending bitonic sort of P2 (power of two) uint64 values in LDS (256 threads).
+__device__ void bitonic_desc(uint64_t* sv, uint32_t P2) {
+  for (uint32_t size = 2; size <= P2; size <<= 1) {
+    for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+      for (uint32_t t = threadIdx.x; t < P2 / 2; t += blockDim.x) {
+        const uint32_t i = 2 * t - (t & (stride - 1)), j = i + stride;
+        const bool desc = (i & size) == 0;
+        const uint64_t x = sv[i], y = sv[j];
+        if ((x < y) == desc) { sv[i] = y; sv[j] = x; }
+      }
+      __syncthreads();
+    }
+  }
+}
+
 // --------------------------------------------------------------------------------------
 // Sampling: level 1 (key >> 19, 4096 bins) and level 2 ((key >> 7) & 0xfff inside the two
-// level-1 bins that hold the bracket ranks).
+// level-1 bins that hold the bracket ranks).  Payload = global atomics only.
 // --------------------------------------------------------------------------------------
 template <int KM, int LEVEL>
 __global__ __launch_bounds__(kBlock) void k_sample(const float* __restrict__ g, SamplePlan P,
@@ -109,11 +131,11 @@ __global__ __launch_bounds__(kBlock) void k_sample(const float* __restrict__ g, 
     if (LEVEL == 2 && hb[b]) atomicAdd(&W.hist2l[b], hb[b]);
   }
   uint32_t* done = LEVEL == 1 ? &S->a_done : &S->b_done;
-  if (!last_block_arrive(done, gridDim.x, &s_flag)) return;
-  // ---- last workgroup: resolve the bracket ranks ----
+  if (!last_block_arrive_sc1(done, gridDim.x, &s_flag)) return;
+  // ---- last workgroup: resolve the bracket ranks (read + clear the histograms) ----
   for (int b = tid; b < kHistBins; b += kBlock) {
-    ha[b] = ld_agent(&gha[b]); gha[b] = 0;
-    if (LEVEL == 2) { hb[b] = ld_agent(&W.hist2l[b]); W.hist2l[b] = 0; }
+    ha[b] = ld_agent(&gha[b]); st_agent(&gha[b], 0u);
+    if (LEVEL == 2) { hb[b] = ld_agent(&W.hist2l[b]); st_agent(&W.hist2l[b], 0u); }
   }
   __syncthreads();
   if (LEVEL == 1) {
@@ -134,18 +156,25 @@ __global__ __launch_bounds__(kBlock) void k_sample(const float* __restrict__ g, 
       find_rank_desc(hb, S->rr_lo, s_tmp, s_out);
       t_lo = (b1_lo << 19) | (s_out[0] << 7);
     }
+    if (tid < kShards) { S->shard_ent[tid] = 0; S->shard_cnd[tid] = 0; }  // k_compact totals
     if (tid == 0) {
-      S->t_lo = t_lo; S->t_hi = t_hi; S->L64 = (uint64_t)t_lo << ib; S->cand_on = 1;
-      S->n_hi = 0; S->n_cand = 0; S->cand_over = 0; S->ent_over = 0;
-      S->e_done = 0; S->e_ticket = 0; S->e_small_n = 0; S->e_status = 0;
+      const uint64_t span = (uint64_t)t_hi - t_lo;          // candidate keys: [t_lo, t_hi]
+      uint32_t sb = 0;
+      while ((span >> sb) >= (uint64_t)kHistBins) ++sb;
+      S->t_lo = t_lo; S->t_hi = t_hi; S->sbin = sb; S->L64 = (uint64_t)t_lo << ib;
+      S->cand_on = 1; S->n_cand = 0; S->cand_over = 0; S->ent_over = 0;
       S->b_done = 0;
       hdr->lower = (uint64_t)t_lo << ib;
     }
   }
 }
 
+
 // --------------------------------------------------------------------------------------
-// k_compact: one pass over g, ordered stream compaction with decoupled look-back.
+// k_compact: one independent workgroup per 8192-element chunk (slotted packet, no global
+// scan).  Element layout: e = i*1024 + w*256 + lane*4 + j (i < 8, w < 4, j < 4): each wave
+// instruction moves 1 KiB contiguous and (i, w, lane, j) order is ascending index order, so
+// ballot + mbcnt + a 32-slot LDS scan give ordered offsets inside the chunk's slot.
 // --------------------------------------------------------------------------------------
 enum Pred : int { kPredKey = 0, kPredMask = 1, kPredBern = 2 };
 
@@ -157,46 +186,37 @@ struct CompactArgs {
   const uint32_t* mask;     // kPredMask
   uint64_t bern_thr;        // kPredBern: keep iff word < thr
   uint32_t nonfinite_keep;  // dropout: dropped inf/NaN are listed as NaN (g * 0 == NaN)
-  uint32_t write_hdr;       // first kernel of a mask pipeline writes the static header
+  uint32_t write_hdr;       // mask pipelines (no earlier kernel) write the static header
   uint32_t* idx;
   float* val;
   uint32_t* bitmap;
-  uint64_t cap;
-  uint32_t* dir;
+  uint32_t* cnt;            // entries per chunk
   fc_packet_hdr* hdr;
   WsPtrs W;
   HdrInit HI;
 };
 
-constexpr uint32_t kSpinLimit = 1u << 22;
-
 template <int KM, int PRED, int FMT>
 __global__ __launch_bounds__(kBlock) void k_compact(CompactArgs a) {
-  __shared__ uint32_t s_wcnt[kVec * kWaves];
-  __shared__ uint32_t s_bex, s_cnt_def, s_cnt_cand, s_cand_base;
-  __shared__ uint64_t s_tk;
+  __shared__ uint32_t s_ent[kSlots], s_cnd[kSlots];
   const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
   TopkState* S = a.W.st;
-  if (tid == 0) {
-    const uint64_t tk = atomicAdd((unsigned long long*)&S->ticket, 1ull);
-    if ((uint32_t)tk == a.nchunks - 1)                    // every ticket handed out
-      atomicExch((unsigned long long*)&S->ticket, ((tk >> 32) + 1) << 32);
-    s_tk = tk; s_cnt_def = 0; s_cnt_cand = 0;
-  }
-  __syncthreads();
-  const uint32_t chunk = (uint32_t)s_tk, epoch = (uint32_t)(s_tk >> 32);
+  const uint32_t chunk = blockIdx.x;
   const uint64_t base = (uint64_t)chunk * kChunk;
+  if (a.write_hdr && chunk == 0 && tid == 0) write_hdr_static(a.hdr, a.HI);  // sole writer
 
   uint64_t L64 = 0;
-  uint32_t t_lo = 0, t_hi = 0xffffffffu, cand_on = 0;
-  if (PRED == kPredKey) { L64 = S->L64; t_lo = S->t_lo; t_hi = S->t_hi; cand_on = S->cand_on; }
+  uint32_t t_lo = 0, t_hi = 0xffffffffu, cand_on = 0, sbin = 0;
+  if (PRED == kPredKey) {
+    L64 = S->L64; t_lo = S->t_lo; t_hi = S->t_hi; cand_on = S->cand_on; sbin = S->sbin;
+  }
 
   float4 x[kVec];
 #pragma unroll
   for (int i = 0; i < kVec; ++i)
     x[i] = load4(a.g, base + (uint64_t)(i * 1024 + w * 256 + lane * 4), a.n);
 
-  uint32_t pbits = 0, cbits = 0, ndef = 0;
+  uint32_t pbits = 0, cbits = 0;   // bit (i*4 + j): listed / candidate (or NaN stand-in)
 #pragma unroll
   for (int i = 0; i < kVec; ++i) {
     const uint64_t e0 = base + (uint64_t)(i * 1024 + w * 256 + lane * 4);
@@ -209,35 +229,42 @@ __global__ __launch_bounds__(kBlock) void k_compact(CompactArgs a) {
     for (int j = 0; j < 4; ++j) {
       const uint64_t e = e0 + j;
       const bool valid = e < a.n;
-      bool p = false;
+      bool p;
       if (PRED == kPredKey) {
         const uint32_t key = u4get(kk, j);
         p = valid && comp_of(key, (uint32_t)e, a.ib) >= L64;
-        ndef += (valid && key > t_hi) ? 1u : 0u;
-        if (valid && cand_on && key >= t_lo && key <= t_hi) cbits |= 1u << (i * 4 + j);
+        if (valid && cand_on && key >= t_lo && key <= t_hi) {
+          cbits |= 1u << (i * 4 + j);
+          atomicAdd(&a.W.chist[(key - t_lo) >> sbin], 1u);
+        }
       } else {
         const bool keep = PRED == kPredMask ? ((mword >> j) & 1u) != 0
                                             : (uint64_t)u4get(kk, j) < a.bern_thr;
         const uint32_t ab = __float_as_uint(f4get(x[i], j)) & 0x7fffffffu;
         const bool nan_standin = a.nonfinite_keep && !keep && ab >= 0x7f800000u;  // g*0 = NaN
         p = valid && (keep || nan_standin);
-        if (valid && nan_standin) cbits |= 1u << (i * 4 + j);   // listed as NaN, not as g
+        if (valid && nan_standin) cbits |= 1u << (i * 4 + j);
       }
       if (p) pbits |= 1u << (i * 4 + j);
     }
   }
 
-  // per-iteration wave ballots -> ordered offsets
-  uint32_t lane_excl[kVec];
+  // per-(i, w) counts (+ bitmap words, natural bit order)
 #pragma unroll
   for (int i = 0; i < kVec; ++i) {
     const uint64_t m0 = __ballot((pbits >> (i * 4 + 0)) & 1u);
     const uint64_t m1 = __ballot((pbits >> (i * 4 + 1)) & 1u);
     const uint64_t m2 = __ballot((pbits >> (i * 4 + 2)) & 1u);
     const uint64_t m3 = __ballot((pbits >> (i * 4 + 3)) & 1u);
-    lane_excl[i] = prefix_count(m0) + prefix_count(m1) + prefix_count(m2) + prefix_count(m3);
-    if (lane == 0)
-      s_wcnt[i * kWaves + w] = __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3);
+    uint32_t nc = 0;
+    if (PRED == kPredKey) {
+      nc = __popcll(__ballot((cbits >> (i * 4 + 0)) & 1u)) + __popcll(__ballot((cbits >> (i * 4 + 1)) & 1u)) +
+           __popcll(__ballot((cbits >> (i * 4 + 2)) & 1u)) + __popcll(__ballot((cbits >> (i * 4 + 3)) & 1u));
+    }
+    if (lane == 0) {
+      s_ent[i * kWaves + w] = __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3);
+      s_cnd[i * kWaves + w] = nc;
+    }
     if (FMT == FC_FMT_BITMAP && lane < 8) {
       const int sh = lane * 8;
       const uint32_t word = spread4((uint32_t)(m0 >> sh)) | (spread4((uint32_t)(m1 >> sh)) << 1) |
@@ -245,133 +272,209 @@ __global__ __launch_bounds__(kBlock) void k_compact(CompactArgs a) {
       a.bitmap[(base + (uint64_t)(i * 1024 + w * 256)) / 32 + lane] = word;
     }
   }
-  if (PRED == kPredKey) {
-    if (ndef) atomicAdd(&s_cnt_def, ndef);
-  }
-  uint32_t my_cand_off = 0;
-  const uint32_t ncand = PRED == kPredKey ? (uint32_t)__popc(cbits) : 0u;
-  if (ncand) my_cand_off = atomicAdd(&s_cnt_cand, ncand);
   __syncthreads();
-
-  if (w == 0) {
-    // (i, w) exclusive scan of the 32 wave counts
-    uint32_t v = lane < kVec * kWaves ? s_wcnt[lane] : 0u, inc = v;
+  if (w == 0) {   // exclusive scan of the 32 slots (lanes 0..31) for both counts
+    const uint32_t ve = lane < kSlots ? s_ent[lane] : 0u, vc = lane < kSlots ? s_cnd[lane] : 0u;
+    uint32_t ie = ve, ic = vc;
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t t = __shfl_up(inc, o, 64);
-      if (lane >= o) inc += t;
+    for (int o = 1; o < 32; o <<= 1) {
+      const uint32_t te = __shfl_up(ie, o, 64), tc = __shfl_up(ic, o, 64);
+      if (lane >= o) { ie += te; ic += tc; }
     }
-    if (lane < kVec * kWaves) s_wcnt[lane] = inc - v;
-    const uint32_t agg = __shfl(inc, 63, 64);
-    // decoupled look-back
-    uint64_t* status = a.W.status;
-    uint32_t excl = 0;
-    if (chunk == 0) {
-      if (lane == 0) st_agent(&status[0], granule(epoch, kFlagInc, agg));
-    } else {
-      if (lane == 0) st_agent(&status[chunk], granule(epoch, kFlagAgg, agg));
-      int64_t jw = (int64_t)chunk - 1;
-      uint32_t spins = 0;
-      const uint32_t ep = epoch & 0x3fffffffu;
-      while (true) {
-        const int64_t p = jw - lane;
-        uint64_t s = granule(epoch, kFlagInc, 0);
-        bool ready = true;
-        if (p >= 0) {
-          s = ld_agent(&status[p]);
-          ready = g_epoch(s) == ep && g_flag(s) != 0;
-        }
-        while (!__all(ready)) {
-          __builtin_amdgcn_s_sleep(1);
-          if (!ready) {
-            s = ld_agent(&status[p]);
-            ready = g_epoch(s) == ep && g_flag(s) != 0;
-          }
-          if (++spins > kSpinLimit) {            // never expected: bounded for safety
-            if (!ready) { s = granule(epoch, kFlagInc, 0); ready = true; atomicOr(&S->err, 1u); }
-          }
-        }
-        const uint64_t incm = __ballot(g_flag(s) == kFlagInc);
-        if (incm) {
-          const int L = __ffsll((long long)incm) - 1;   // nearest inclusive predecessor
-          excl += wave_sum(lane <= L ? g_val(s) : 0u);
-          break;
-        }
-        excl += wave_sum(g_val(s));
-        jw -= 64;
-      }
-      if (lane == 0) st_agent(&status[chunk], granule(epoch, kFlagInc, excl + agg));
-    }
-    if (lane == 0) {
-      s_bex = excl;
-      a.dir[chunk] = excl;
-      if (chunk == a.nchunks - 1) {             // the ONLY writer of hdr in this launch
-        if (a.write_hdr) write_hdr_static(a.hdr, a.HI);
-        a.dir[a.nchunks] = excl + agg;
-        a.hdr->n_entries = excl + agg;
-        if ((uint64_t)excl + agg > a.cap) {
-          a.hdr->status = FC_STATUS_OVERFLOW;
-          if (PRED == kPredKey) atomicOr(&S->ent_over, 1u);
-        }
-      }
+    if (lane < kSlots) { s_ent[lane] = ie - ve; s_cnd[lane] = ic - vc; }
+    if (lane == kSlots - 1) {
+      a.cnt[chunk] = ie;
       if (PRED == kPredKey) {
-        if (s_cnt_def) atomicAdd(&S->n_hi, s_cnt_def);
-        if (s_cnt_cand) s_cand_base = atomicAdd(&S->n_cand, s_cnt_cand);
+        a.W.ccnt[chunk] = ic;
+        atomicAdd(&S->shard_ent[chunk % kShards], ie);
+        if (ic) atomicAdd(&S->shard_cnd[chunk % kShards], ic);
       }
     }
   }
   __syncthreads();
 
-  // candidates (unordered; the engine is order-free because comps are unique)
-  if (PRED == kPredKey && ncand) {
-    uint64_t pos = (uint64_t)s_cand_base + my_cand_off;
-#pragma unroll
-    for (int i = 0; i < kVec; ++i) {
-      const uint64_t e0 = base + (uint64_t)(i * 1024 + w * 256 + lane * 4);
-      const uint4 kk = keys4<KM>(x[i], e0, a.seed, a.offset);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if ((cbits >> (i * 4 + j)) & 1u) {
-          if (pos < a.W.cand_cap) a.W.cand[pos] = comp_of(u4get(kk, j), (uint32_t)(e0 + j), a.ib);
-          else atomicOr(&S->cand_over, 1u);
-          ++pos;
-        }
-      }
-    }
-  }
-
-  // ordered entry writes
-  const uint32_t bex = s_bex;
+  const uint64_t slot = base;                     // entries slot of this chunk
+  const uint64_t cslot = (uint64_t)chunk * kCandSlot;
 #pragma unroll
   for (int i = 0; i < kVec; ++i) {
-    uint64_t pos = (uint64_t)bex + s_wcnt[i * kWaves + w] + lane_excl[i];
     const uint64_t e0 = base + (uint64_t)(i * 1024 + w * 256 + lane * 4);
+    const uint32_t lo = prefix_count(__ballot((pbits >> (i * 4 + 0)) & 1u)) +
+                        prefix_count(__ballot((pbits >> (i * 4 + 1)) & 1u)) +
+                        prefix_count(__ballot((pbits >> (i * 4 + 2)) & 1u)) +
+                        prefix_count(__ballot((pbits >> (i * 4 + 3)) & 1u));
+    uint32_t pos = s_ent[i * kWaves + w] + lo;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       if ((pbits >> (i * 4 + j)) & 1u) {
-        if (pos < a.cap) {
-          float v = f4get(x[i], j);
-          if (PRED != kPredKey && ((cbits >> (i * 4 + j)) & 1u)) v = __uint_as_float(0x7fc00000u);
-          if (FMT == FC_FMT_IDXVAL) a.idx[pos] = (uint32_t)(e0 + j);
-          a.val[pos] = v;
-        }
+        float v = f4get(x[i], j);
+        if (PRED != kPredKey && ((cbits >> (i * 4 + j)) & 1u)) v = __uint_as_float(0x7fc00000u);
+        if (FMT == FC_FMT_IDXVAL) a.idx[slot + pos] = (uint32_t)(e0 + j);
+        a.val[slot + pos] = v;
         ++pos;
+      }
+    }
+    if (PRED == kPredKey && cbits) {
+      const uint32_t lc = prefix_count(__ballot((cbits >> (i * 4 + 0)) & 1u)) +
+                          prefix_count(__ballot((cbits >> (i * 4 + 1)) & 1u)) +
+                          prefix_count(__ballot((cbits >> (i * 4 + 2)) & 1u)) +
+                          prefix_count(__ballot((cbits >> (i * 4 + 3)) & 1u));
+      uint32_t cpos = s_cnd[i * kWaves + w] + lc;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if ((cbits >> (i * 4 + j)) & 1u) {
+          const uint64_t e = e0 + j;
+          if (cpos < (uint32_t)kCandSlot)
+            a.W.cand[cslot + cpos] = comp_of(key1<KM>(f4get(x[i], j), e, a.seed, a.offset), (uint32_t)e, a.ib);
+          ++cpos;
+        }
       }
     }
   }
 }
 
 // --------------------------------------------------------------------------------------
-// k_engine: one radix / collect pass of the exact selection of the rank-th largest comp.
+// k_resolve: exact T64 from the bracket's candidates (fast path, one launch).
+//   totals from the sharded counters -> rank r = k - #(key > t_hi) -> histogram bin beta
+//   holding rank r -> every workgroup gathers its chunks' candidates that fall in beta
+//   (candidate slot, or the entries slot when the chunk overflowed its candidate slot) ->
+//   the last workgroup sorts the <= 4096 survivors in LDS and picks T64.
+// --------------------------------------------------------------------------------------
+struct ResolveArgs {
+  uint32_t ib, nchunks;
+  uint64_t k;
+  const uint32_t* idx;      // packet (for overflowed candidate slots)
+  const float* val;
+  const uint32_t* cnt;
+  uint64_t seed, offset;
+  uint32_t key_mode;
+  fc_packet_hdr* hdr;
+  WsPtrs W;
+};
+
+constexpr int kResolveChunksMax = 2048;   // chunks per workgroup handled through LDS sizes
+
+__global__ __launch_bounds__(kBlock) void k_resolve(ResolveArgs a) {
+  __shared__ uint64_t sv[kSmallCap];                      // 32 KiB: histogram, then sort
+  __shared__ uint32_t s_pre[kResolveChunksMax + 1];       // per-chunk gather sizes (prefix)
+  __shared__ uint32_t s_tmp[8], s_out[4], s_flag, s_cnt, s_base, s_tot[2];
+  uint32_t* h = reinterpret_cast<uint32_t*>(sv);          // 4096 bins = 16 KiB
+  TopkState* S = a.W.st;
+  const int tid = threadIdx.x;
+  // ---- totals (sharded counters written by k_compact) ----
+  if (tid < 2) s_tot[tid] = 0;
+  __syncthreads();
+  if (tid < kShards) {
+    atomicAdd(&s_tot[0], S->shard_ent[tid]);
+    atomicAdd(&s_tot[1], S->shard_cnd[tid]);
+  }
+  __syncthreads();
+  const uint32_t n_ent = s_tot[0], n_cand = s_tot[1];
+  const uint32_t t_lo = S->t_lo, t_hi = S->t_hi, sbin = S->sbin;
+  const uint32_t n_hi = n_ent - n_cand;                   // listed above the bracket
+  const bool bad = S->err || n_cand > n_ent || (uint64_t)n_ent < a.k || (uint64_t)n_hi > a.k;
+  const uint32_t rank = bad ? 0u : (uint32_t)(a.k - n_hi);
+  bool retry = bad;
+  uint32_t beta = 0, r_in = 1, cnt_beta = 0;
+  if (!bad && rank > 0) {
+    for (int b = tid; b < kHistBins; b += kBlock) h[b] = a.W.chist[b];
+    __syncthreads();
+    find_rank_desc(h, rank, s_tmp, s_out);
+    beta = s_out[0]; r_in = s_out[1]; cnt_beta = h[beta];
+    retry = cnt_beta > (uint32_t)kSmallCap || cnt_beta < r_in;
+    __syncthreads();
+  }
+  const uint32_t per = (a.nchunks + gridDim.x - 1) / gridDim.x;
+  if (!bad && rank > 0 && !retry && per <= (uint32_t)kResolveChunksMax) {
+    // chunk range of this workgroup; gather sizes (candidate slot or, overflowed, entries)
+    const uint32_t c0 = blockIdx.x * per;
+    const uint32_t c1 = min(c0 + per, a.nchunks);
+    const uint32_t nc = c1 > c0 ? c1 - c0 : 0u;
+    uint32_t carry = 0;
+    for (uint32_t b0 = 0; b0 < nc; b0 += kBlock) {
+      const uint32_t c = c0 + b0 + tid;
+      uint32_t sz = 0;
+      if (b0 + tid < nc) {
+        const uint32_t cc = a.W.ccnt[c];
+        sz = cc <= (uint32_t)kCandSlot ? cc : a.cnt[c];
+      }
+      uint32_t tot;
+      const uint32_t ex = block_excl_scan(sz, s_tmp, &tot);
+      if (b0 + tid < nc) s_pre[b0 + tid] = carry + ex;
+      carry += tot;
+    }
+    if (tid == 0) { s_pre[nc] = carry; s_cnt = 0; }
+    __syncthreads();
+    // gather bin beta into the LDS list (sv reused after the histogram)
+    for (uint32_t j = tid; j < carry; j += kBlock) {
+      uint32_t lo = 0, hi = nc;                       // find chunk: s_pre[lo] <= j < s_pre[lo+1]
+      while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (s_pre[mid] <= j) lo = mid; else hi = mid; }
+      const uint32_t c = c0 + lo, r = j - s_pre[lo];
+      uint64_t v;
+      if (a.W.ccnt[c] <= (uint32_t)kCandSlot) {
+        v = a.W.cand[(uint64_t)c * kCandSlot + r];
+      } else {
+        const uint64_t p = (uint64_t)c * kChunk + r;
+        const uint32_t id = a.idx[p];
+        const uint32_t key = a.key_mode == FC_KEY_PHILOX ? (philox_word(id, a.seed, a.offset) >> 1)
+                                                         : mag_key(a.val[p]);
+        v = (key >= t_lo && key <= t_hi) ? comp_of(key, id, a.ib) : ~0ull;
+      }
+      if (v != ~0ull && ((((uint32_t)(v >> a.ib)) - t_lo) >> sbin) == beta) {
+        const uint32_t q = atomicAdd(&s_cnt, 1u);
+        if (q < (uint32_t)kSmallCap) sv[q] = v;
+      }
+    }
+    __syncthreads();
+    if (tid == 0 && s_cnt) s_base = atomicAdd(&S->small_n, min(s_cnt, (uint32_t)kSmallCap));
+    __syncthreads();
+    const uint32_t mine = min(s_cnt, (uint32_t)kSmallCap);
+    for (uint32_t q = tid; q < mine; q += kBlock)
+      if (s_base + q < (uint32_t)kSmallCap) st_agent(&a.W.small[s_base + q], sv[q]);
+  } else if (!bad && rank > 0 && !retry) {
+    retry = true;                                     // > 2048 chunks per group: exact path
+  }
+  if (!last_block_arrive_sc1(&S->r_done, gridDim.x, &s_flag)) return;
+  // ---- last workgroup ----
+  uint64_t T = 0;
+  uint32_t status = FC_STATUS_OK;
+  if (retry) {
+    status = FC_STATUS_RETRY_EXACT;
+  } else if (a.k == 0) {
+    T = kSelectNothing;
+  } else if (rank == 0) {
+    T = ((uint64_t)t_hi + 1) << a.ib;                     // exactly the definite set
+  } else {
+    uint32_t P2 = 1;
+    while (P2 < cnt_beta) P2 <<= 1;
+    __syncthreads();
+    for (uint32_t i = tid; i < P2; i += kBlock) sv[i] = i < cnt_beta ? ld_agent(&a.W.small[i]) : 0ull;
+    __syncthreads();
+    bitonic_desc(sv, P2);
+    T = sv[r_in - 1];
+  }
+  __syncthreads();
+  for (int b = tid; b < kHistBins; b += kBlock) a.W.chist[b] = 0;   // for the next call
+  if (tid == 0) {
+    a.hdr->thresh = T;
+    a.hdr->n_entries = n_ent;
+    if (status != FC_STATUS_OK) a.hdr->status = status;
+    a.hdr->n_definite = n_hi;
+    a.hdr->n_cand = n_cand;
+    S->small_n = 0; S->r_done = 0;
+  }
+}
+
+
+// --------------------------------------------------------------------------------------
+// k_engine: exact pipeline — one 12-bit radix (or final LDS-sort) pass of the selection of
+// the k-th largest comp over g itself.  Runs BEFORE k_compact (which then lists exactly
+// comp >= T64).  Used for trivial k and whenever the sampled bracket reports RETRY.
 // --------------------------------------------------------------------------------------
 struct EngineArgs {
-  const float* g;           // src 2 (dense)
+  const float* g;
   uint64_t n;
-  const uint32_t* idx;      // src 1 (packet entries)
-  const float* val;
   uint32_t ib;
-  uint32_t first;           // 1: initialise the state (every block computes it identically)
-  uint32_t exact;           // 1: exact pipeline (engine runs BEFORE k_compact)
+  uint32_t first;
   uint64_t k;
   uint64_t seed, offset;
   fc_packet_hdr* hdr;
@@ -381,80 +484,40 @@ struct EngineArgs {
 
 struct EngState {
   uint64_t prefix;
-  uint32_t shift, rank, matched, done, src, status;
+  uint32_t shift, rank, matched, done, status;
   uint64_t result;
 };
 
-__device__ __forceinline__ int clz64(uint64_t x) { return x ? __clzll((long long)x) : 64; }
-
-// Every field is assigned on every path (a partially initialised state let hipcc fold the
-// rank of the cand_over path into an undefined register — see DESIGN.md §Lessons).
-template <int KM>
-__device__ __forceinline__ EngState engine_init(const EngineArgs& a) {
-  TopkState* S = a.W.st;
-  const uint32_t top = 31 + a.ib;          // comps < 2^(31+IB)
-  const uint32_t k32 = (uint32_t)a.k;
-  if (a.exact) {
-    const uint32_t done = (a.k == 0 || a.k >= a.n) ? 1u : 0u;
-    const uint64_t res = a.k == 0 ? kSelectNothing : 0ull;
-    return EngState{0ull, top, k32, (uint32_t)a.n, done, 2u, (uint32_t)FC_STATUS_OK, res};
-  }
-  const uint32_t n_hi = S->n_hi, n_cand = S->n_cand, t_lo = S->t_lo, t_hi = S->t_hi;
-  const uint32_t n_ent = a.hdr->n_entries;
-  const bool retry = S->ent_over != 0 || S->err != 0 || (uint64_t)n_hi + n_cand < a.k;
-  if (a.k == 0)
-    return EngState{0ull, top, 0u, 0u, 1u, 2u, (uint32_t)FC_STATUS_OK, kSelectNothing};
-  if (retry)
-    return EngState{0ull, top, k32, 0u, 1u, 2u, (uint32_t)FC_STATUS_RETRY_EXACT, 0ull};
-  const bool use_entries = n_hi > a.k || S->cand_over != 0;   // the listed superset
-  if (use_entries)
-    return EngState{0ull, top, k32, n_ent, 0u, 1u, (uint32_t)FC_STATUS_OK, 0ull};
-  const uint32_t rank = k32 - n_hi;
-  if (rank == 0)
-    return EngState{0ull, top, 0u, n_cand, 1u, 0u, (uint32_t)FC_STATUS_OK,
-                    ((uint64_t)t_hi + 1) << a.ib};
-  const uint64_t lo = (uint64_t)t_lo << a.ib;
-  const uint64_t hi = ((uint64_t)t_hi << a.ib) | ((1ull << a.ib) - 1);
-  const uint32_t sh = 64 - clz64(lo ^ hi);
-  const uint64_t prefix = sh >= 64 ? 0ull : (lo >> sh) << sh;
-  return EngState{prefix, sh, rank, n_cand, 0u, 0u, (uint32_t)FC_STATUS_OK, 0ull};
-}
-
-template <int KM>
-__device__ __forceinline__ uint64_t engine_comp(const EngineArgs& a, uint32_t src, uint64_t i) {
-  if (src == 0) return a.W.cand[i];
-  if (src == 1) {
-    const uint32_t id = a.idx[i];
-    return comp_of(key1<KM>(a.val[i], id, a.seed, a.offset), id, a.ib);
-  }
-  return comp_of(key1<KM>(a.g[i], i, a.seed, a.offset), (uint32_t)i, a.ib);
-}
-
 template <int KM>
 __global__ __launch_bounds__(kBlock) void k_engine(EngineArgs a) {
-  __shared__ uint32_t h[kHistBins];            // reused as the bitonic buffer (16 KiB)
+  __shared__ uint64_t sv[kSmallCap];                      // 32 KiB, also the histogram
   __shared__ uint32_t s_tmp[8], s_out[4], s_flag, s_cnt, s_base;
+  uint32_t* h = reinterpret_cast<uint32_t*>(sv);
   TopkState* S = a.W.st;
   const int tid = threadIdx.x;
-  const EngState E0 = a.first ? engine_init<KM>(a)
-                              : EngState{S->e_prefix, S->e_shift, S->e_rank, S->e_matched,
-                                         S->e_done, S->e_src, S->e_status, S->e_prefix};
+  // every field assigned on every path (a partially initialised state once let hipcc fold
+  // a rank into an undefined register: DESIGN.md §Lessons)
+  const uint32_t top = 31 + a.ib;
+  const EngState E0 =
+      a.first ? EngState{0ull, top, (uint32_t)a.k, (uint32_t)a.n,
+                         (a.k == 0 || a.k >= a.n) ? 1u : 0u, (uint32_t)FC_STATUS_OK,
+                         a.k == 0 ? kSelectNothing : 0ull}
+              : EngState{S->e_prefix, S->e_shift, S->e_rank, S->e_matched, S->e_done,
+                         S->e_status, S->e_prefix};
   EngState E = E0;
-  if (!a.first && E.done) return;             // resolved by an earlier pass
+  if (!a.first && E.done) return;                         // resolved by an earlier pass
 
-  uint64_t cnt = E.src == 0 ? (uint64_t)min(S->n_cand, (uint32_t)a.W.cand_cap)
-               : E.src == 1 ? (uint64_t)a.hdr->n_entries : a.n;
   const bool collect = !E.done && E.matched <= (uint32_t)kSmallCap;
   const uint32_t D = E.shift < (uint32_t)kHistBits ? E.shift : (uint32_t)kHistBits;
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  const uint64_t hi_part = E.prefix >> E.shift;
   if (!E.done) {
     for (int b = tid; b < kHistBins; b += kBlock) h[b] = 0;
     if (tid == 0) s_cnt = 0;
     __syncthreads();
-    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-    const uint64_t hi_part = E.prefix >> E.shift;
     if (!collect) {
-      for (uint64_t i = (uint64_t)blockIdx.x * kBlock + tid; i < cnt; i += stride) {
-        const uint64_t v = engine_comp<KM>(a, E.src, i);
+      for (uint64_t i = (uint64_t)blockIdx.x * kBlock + tid; i < a.n; i += stride) {
+        const uint64_t v = comp_of(key1<KM>(a.g[i], i, a.seed, a.offset), (uint32_t)i, a.ib);
         if ((v >> E.shift) == hi_part)
           atomicAdd(&h[(uint32_t)(v >> (E.shift - D)) & ((1u << D) - 1)], 1u);
       }
@@ -462,31 +525,31 @@ __global__ __launch_bounds__(kBlock) void k_engine(EngineArgs a) {
       for (int b = tid; b < kHistBins; b += kBlock)
         if (h[b]) atomicAdd(&a.W.ehist[b], h[b]);
     } else {
-      // gather the <= kSmallCap survivors (order free)
       uint32_t mine = 0;
-      for (uint64_t i = (uint64_t)blockIdx.x * kBlock + tid; i < cnt; i += stride) {
-        const uint64_t v = engine_comp<KM>(a, E.src, i);
+      for (uint64_t i = (uint64_t)blockIdx.x * kBlock + tid; i < a.n; i += stride) {
+        const uint64_t v = comp_of(key1<KM>(a.g[i], i, a.seed, a.offset), (uint32_t)i, a.ib);
         mine += (v >> E.shift) == hi_part ? 1u : 0u;
       }
-      uint32_t off = mine ? atomicAdd(&s_cnt, mine) : 0u;
+      const uint32_t off = mine ? atomicAdd(&s_cnt, mine) : 0u;
       __syncthreads();
-      if (tid == 0 && s_cnt) s_base = atomicAdd(&S->e_small_n, s_cnt);
+      if (tid == 0 && s_cnt) s_base = atomicAdd(&S->small_n, s_cnt);
       __syncthreads();
       if (mine) {
         uint32_t pos = s_base + off;
-        for (uint64_t i = (uint64_t)blockIdx.x * kBlock + tid; i < cnt; i += stride) {
-          const uint64_t v = engine_comp<KM>(a, E.src, i);
-          if ((v >> E.shift) == hi_part && pos < (uint32_t)kSmallCap) a.W.small[pos++] = v;
+        for (uint64_t i = (uint64_t)blockIdx.x * kBlock + tid; i < a.n; i += stride) {
+          const uint64_t v = comp_of(key1<KM>(a.g[i], i, a.seed, a.offset), (uint32_t)i, a.ib);
+          if ((v >> E.shift) == hi_part && pos < (uint32_t)kSmallCap) st_agent(&a.W.small[pos++], v);
         }
       }
     }
   }
-  if (!last_block_arrive(&S->e_ticket, gridDim.x, &s_flag)) return;
+  if (!last_block_arrive_sc1(&S->e_ticket, gridDim.x, &s_flag)) return;
 
   // ---- last workgroup: advance the state ----
   if (!E.done) {
     if (!collect) {
-      for (int b = tid; b < kHistBins; b += kBlock) { h[b] = ld_agent(&a.W.ehist[b]); a.W.ehist[b] = 0; }
+      __syncthreads();
+      for (int b = tid; b < kHistBins; b += kBlock) { h[b] = ld_agent(&a.W.ehist[b]); st_agent(&a.W.ehist[b], 0u); }
       __syncthreads();
       find_rank_desc(h, E.rank, s_tmp, s_out);
       const uint32_t d = s_out[0];
@@ -496,24 +559,13 @@ __global__ __launch_bounds__(kBlock) void k_engine(EngineArgs a) {
       E.matched = h[d];
       if (E.shift == 0) { E.done = 1; E.result = E.prefix; }
     } else {
-      // bitonic sort (descending) of the survivors in LDS (as uint64 pairs in h[])
-      uint64_t* sv = reinterpret_cast<uint64_t*>(h);
       const uint32_t m = E.matched;
       uint32_t P2 = 1;
       while (P2 < m) P2 <<= 1;
+      __syncthreads();
       for (uint32_t i = tid; i < P2; i += kBlock) sv[i] = i < m ? ld_agent(&a.W.small[i]) : 0ull;
       __syncthreads();
-      for (uint32_t size = 2; size <= P2; size <<= 1) {
-        for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
-          for (uint32_t t = tid; t < P2 / 2; t += kBlock) {
-            const uint32_t i = 2 * t - (t & (stride - 1)), j = i + stride;
-            const bool desc = (i & size) == 0;
-            const uint64_t x = sv[i], y = sv[j];
-            if ((x < y) == desc) { sv[i] = y; sv[j] = x; }
-          }
-          __syncthreads();
-        }
-      }
+      bitonic_desc(sv, P2);
       if (E.rank >= 1 && E.rank <= m) E.result = sv[E.rank - 1];
       else E.status = FC_STATUS_TIMEOUT;   // inconsistent state: never expected
       E.done = 1;
@@ -521,22 +573,18 @@ __global__ __launch_bounds__(kBlock) void k_engine(EngineArgs a) {
     }
   }
   if (tid == 0) {
-    if (a.first && a.exact) write_hdr_static(a.hdr, a.HI);   // sole hdr writer of this launch
+    if (a.first) write_hdr_static(a.hdr, a.HI);   // sole hdr writer of this launch
     S->e_prefix = E.prefix; S->e_shift = E.shift; S->e_rank = E.rank; S->e_matched = E.matched;
-    S->e_done = E.done; S->e_src = E.src; S->e_status = E.status;
-    S->e_ticket = 0; S->e_small_n = 0;
+    S->e_done = E.done; S->e_status = E.status;
+    S->e_ticket = 0; S->small_n = 0;
     if (E.done) {
       a.hdr->thresh = E.result;
+      a.hdr->lower = E.result;
+      a.hdr->n_entries = (uint32_t)a.k;           // exactly comp >= T64 gets listed
       if (E.status != FC_STATUS_OK) a.hdr->status = E.status;
-      if (!a.exact) {
-        a.hdr->n_definite = S->n_hi; a.hdr->n_cand = S->n_cand;
-        S->n_hi = 0; S->n_cand = 0; S->cand_over = 0; S->ent_over = 0;
-      } else {
-        // exact pipeline: k_compact runs next and lists exactly comp >= T64
-        S->L64 = E.result; S->t_lo = (uint32_t)(E.result >> a.ib); S->t_hi = 0xffffffffu;
-        S->cand_on = 0; S->n_hi = 0; S->n_cand = 0; S->cand_over = 0; S->ent_over = 0;
-        a.hdr->lower = E.result;
-      }
+      // k_compact runs next and lists exactly comp >= T64
+      S->L64 = E.result; S->t_lo = (uint32_t)(E.result >> a.ib); S->t_hi = 0xffffffffu;
+      S->cand_on = 0; S->sbin = 0; S->n_cand = 0; S->cand_over = 0; S->ent_over = 0;
     }
   }
 }

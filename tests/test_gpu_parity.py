@@ -182,8 +182,11 @@ def test_top_128M_properties():
     assert torch.equal(out[nz], g[nz])                       # exact copies
     a = g.abs()
     assert float(a[nz].min()) >= float(a[~nz].max())         # every kept >= every dropped
-    idx = pkt.idx[: h.n_entries].to(torch.int64)
-    assert bool((idx[1:] > idx[:-1]).all())                  # ascending packet
+    pos = torch.arange(pkt.capacity, device="cuda")
+    listed = (pos % 8192) < pkt.cnt.to(torch.int64)[pos // 8192]
+    idx = pkt.idx[listed].to(torch.int64)
+    assert idx.numel() == h.n_entries
+    assert bool((idx[1:] > idx[:-1]).all())                  # ascending packet (slot order)
     # slack stays small (the packet carries few unselected entries)
     assert h.n_entries - k < 0.06 * k
 

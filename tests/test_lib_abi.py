@@ -54,16 +54,15 @@ def test_struct_layouts():
     assert ctypes.sizeof(_lib.PacketHdr) == 96
     assert ctypes.sizeof(_lib.PacketView) == 48
     assert _lib.PacketHdr.p.offset == 64 and _lib.PacketHdr.seed.offset == 48
+    assert _lib.PacketView.cnt.offset == 24 and _lib.PacketView.weight.offset == 40
 
 
 def test_sizes_are_host_functions(lib):
     assert lib.fc_num_chunks(1) == 1 and lib.fc_num_chunks(8192) == 1
     assert lib.fc_num_chunks(8193) == 2
     assert lib.fc_workspace_bytes(1 << 27) > 8 * lib.fc_num_chunks(1 << 27)
-    n, k = 134_217_728, 13_421_773
-    cap = lib.fc_topk_capacity(n, k)
-    assert k < cap < k * 1.15
-    assert lib.fc_topk_capacity(1000, 100) == 1000
+    assert lib.fc_packet_capacity(134_217_728) == 134_217_728
+    assert lib.fc_packet_capacity(1000) == 8192
 
 
 def test_argument_errors_do_not_touch_gpu(lib):
