@@ -6,6 +6,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <vector>
 
 // Part of the unity build (fedcodec.hip): the kernels and their argument structs from
@@ -59,6 +60,18 @@ static WsPtrs ws_ptrs(void* ws, uint64_t n) {
 
 // Stratified sample + bracket ranks.  Full sample for n <= 1 M (exact bracket); otherwise
 // 64..1024 segments of 1024 (n/32 .. 1 M keys) and a +-6 sigma binomial margin.
+// Persistent decode grid: every workgroup resident (4 per CU at ~38 KiB LDS), each walking
+// ceil(chunks / grid) chunks.  FC_DECODE_GRID overrides (tuning only).
+static uint32_t decode_grid(uint64_t n) {
+  static const uint32_t forced = [] {
+    const char* e = getenv("FC_DECODE_GRID");
+    return e ? (uint32_t)atoi(e) : 0u;
+  }();
+  uint32_t g = forced ? forced : 256u * kDecBlocksPerCU;
+  const uint32_t nch = num_chunks(n);
+  return g < nch ? g : nch;
+}
+
 static SamplePlan make_plan(uint64_t n, uint64_t k) {
   SamplePlan P;
   memset(&P, 0, sizeof P);
@@ -137,9 +150,9 @@ static int launch_engine(int key_mode, const EngineArgs& base, int passes, hipSt
 static int launch_compact_key(int key_mode, const CompactArgs& a, hipStream_t s) {
   TimedLaunch t(FC_TIME_COMPACT, s);
   if (key_mode == FC_KEY_PHILOX)
-    hipLaunchKernelGGL((k_compact<kKeyPhilox, kPredKey, FC_FMT_IDXVAL>), dim3(a.nchunks), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL((k_compact<kKeyPhilox, kPredKey, FC_FMT_IDXVAL>), dim3(a.nchunks), dim3(kCBlock), 0, s, a);
   else
-    hipLaunchKernelGGL((k_compact<kKeyMag, kPredKey, FC_FMT_IDXVAL>), dim3(a.nchunks), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL((k_compact<kKeyMag, kPredKey, FC_FMT_IDXVAL>), dim3(a.nchunks), dim3(kCBlock), 0, s, a);
   FC_LAUNCHED("k_compact");
   return FC_OK;
 }
@@ -251,7 +264,7 @@ int fc_topk_encode(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
   const SamplePlan P = make_plan(n, k);
-  const uint32_t sgrid = P.nseg < 256 ? P.nseg : 256;
+  const uint32_t sgrid = (P.nseg + kSampleSegs - 1) / kSampleSegs;   // <= 256
   {
     TimedLaunch t(FC_TIME_SAMPLE, s);
     if (key_mode == FC_KEY_PHILOX) {
@@ -304,7 +317,7 @@ int fc_mask_encode(const float* g, uint64_t n, int codec, const uint32_t* mask_b
   a.write_hdr = 1; a.idx = idx; a.val = val; a.bitmap = bitmap; a.cnt = cnt;
   a.hdr = hdr; a.W = ws_ptrs(ws, n); a.HI = hi;
   hipStream_t s = (hipStream_t)stream;
-  const dim3 grid(a.nchunks), blk(kBlock);
+  const dim3 grid(a.nchunks), blk(kCBlock);
   TimedLaunch t(FC_TIME_COMPACT, s);
   if (mask_bits) {
     if (format == FC_FMT_BITMAP) hipLaunchKernelGGL((k_compact<kKeyMag, kPredMask, FC_FMT_BITMAP>), grid, blk, 0, s, a);
@@ -330,7 +343,7 @@ int fc_decode_dense(const fc_packet_view* pkt, int format, uint64_t n, void* out
   memset(&a, 0, sizeof a);
   a.views = nullptr; a.one = *pkt; a.m = 1; a.n = n; a.out = out;
   hipStream_t s = (hipStream_t)stream;
-  const dim3 grid(num_chunks(n)), blk(kBlock);
+  const dim3 grid(decode_grid(n)), blk(kDBlock);
   TimedLaunch t(FC_TIME_DECODE, s);
   if (format == FC_FMT_IDXVAL) {
     if (out_f64) hipLaunchKernelGGL((k_decode<FC_FMT_IDXVAL, false, true>), grid, blk, 0, s, a);
@@ -350,15 +363,19 @@ int fc_decode_accumulate(const fc_packet_view* views_dev, int m, int format, uin
   FC_CHECK(n >= 1 && n <= 0xffffffffull, "bad n");
   FC_CHECK(format == FC_FMT_IDXVAL || format == FC_FMT_BITMAP, "bad format %d", format);
   FC_CHECK(((uintptr_t)acc & 15) == 0, "acc must be 16-byte aligned");
-  DecodeArgs a;
-  memset(&a, 0, sizeof a);
-  a.views = views_dev; a.m = m; a.n = n; a.out = acc;
   hipStream_t s = (hipStream_t)stream;
-  const dim3 grid(num_chunks(n)), blk(kBlock);
-  TimedLaunch t(FC_TIME_DECODE, s);
-  if (format == FC_FMT_IDXVAL) hipLaunchKernelGGL((k_decode<FC_FMT_IDXVAL, true, false>), grid, blk, 0, s, a);
-  else hipLaunchKernelGGL((k_decode<FC_FMT_BITMAP, true, false>), grid, blk, 0, s, a);
-  FC_LAUNCHED("k_decode(acc)");
+  const dim3 grid(decode_grid(n)), blk(kDBlock);
+  // <= kDecMaxM packets per launch; later launches continue the same left-to-right sum
+  for (int m0 = 0; m0 < m; m0 += kDecMaxM) {
+    DecodeArgs a;
+    memset(&a, 0, sizeof a);
+    a.views = views_dev + m0; a.m = std::min(m - m0, kDecMaxM); a.acc_in = m0 > 0;
+    a.n = n; a.out = acc;
+    TimedLaunch t(FC_TIME_DECODE, s);
+    if (format == FC_FMT_IDXVAL) hipLaunchKernelGGL((k_decode<FC_FMT_IDXVAL, true, false>), grid, blk, 0, s, a);
+    else hipLaunchKernelGGL((k_decode<FC_FMT_BITMAP, true, false>), grid, blk, 0, s, a);
+    FC_LAUNCHED("k_decode(acc)");
+  }
   return FC_OK;
 }
 

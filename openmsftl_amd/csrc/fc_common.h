@@ -91,9 +91,35 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
   return v;
 }
 
+// Inclusive prefix sum over the 64 lanes of a wave with DPP (GFX9 row_shr / row_bcast):
+// 6 fused adds, no LDS.  Lanes whose DPP source is out of range add 0.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return x;
+}
+__device__ __forceinline__ uint32_t lane63(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+
 // float4 load of elements [e, e+4) with zero fill past n (16-B aligned base required)
+#ifndef FC_NT_LOADS
+#define FC_NT_LOADS 1
+#endif
 __device__ __forceinline__ float4 load4(const float* __restrict__ g, uint64_t e, uint64_t n) {
-  if (e + 4 <= n) return *reinterpret_cast<const float4*>(g + e);
+  if (e + 4 <= n) {
+#if FC_NT_LOADS
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(g + e));
+    return make_float4(v.x, v.y, v.z, v.w);
+#else
+    return *reinterpret_cast<const float4*>(g + e);
+#endif
+  }
   float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
   if (e + 0 < n) r.x = g[e + 0];
   if (e + 1 < n) r.y = g[e + 1];

@@ -11,6 +11,8 @@
 // register accumulator exactly as gar.py:44 does on the dense G:
 //   acc = fl(w_0 * d_0);  acc = fl(acc + fl(w_i * d_i))   (no FMA: __fmul_rn / __fadd_rn)
 // so the FedAVG of M packets reads each packet once and writes the aggregate once.
+#include <type_traits>
+
 #include "fc_state.h"
 
 namespace fc {
@@ -73,105 +75,279 @@ __device__ __forceinline__ void store_out(OutT* out, uint64_t e, uint64_t n, con
 struct DecodeArgs {
   const fc_packet_view* views;  // device array (ACC) — or nullptr with `one` filled
   fc_packet_view one;
-  int m;
+  int m;                        // packets in this launch (<= kDecMaxM)
+  int acc_in;                   // ACC: continue an earlier launch's sum held in `out`
   uint64_t n;
   void* out;
 };
 
+constexpr int kDBlock = 256;                   // decode workgroup (4 waves)
+constexpr int kDVec = kChunk / (kDBlock * 4);  // 8 float4 per thread: e = i*1024 + w*256 + lane*4
+constexpr int kDecR = 4;                       // slot entries per thread per item (1024 / chunk)
+#ifndef FC_DEC_GROUP
+#define FC_DEC_GROUP 4
+#endif
+constexpr int kDecGroup = FC_DEC_GROUP;        // items whose loads are issued together
+constexpr int kDecMaxM = 64;                   // packets per launch (the host splits larger batches)
+constexpr int kDecBlocksPerCU = 4;
+
+// Pointers read back from memory are generic (flat) to the compiler; loads through these
+// casts are plain global loads with a scalar base.
+typedef __attribute__((address_space(1))) const float gf32;
+typedef __attribute__((address_space(1))) const uint32_t gu32;
+
+// Per-packet record staged in LDS once per workgroup (no per-step header/view loads).
+struct DecMeta {
+  const uint32_t* idx;        // FC_FMT_IDXVAL: idx; FC_FMT_BITMAP: bitmap
+  const float* val;
+  const uint32_t* cnt;
+  uint64_t seed, offset;      // rand-k (PHILOX) keys for the slack filter
+  double p;                   // dropout-unbiased scale
+  uint64_t thresh;
+  float w;
+  uint32_t flags;             // ib | codec << 8 | key_mode << 16
+};
+
+// One "item" = one packet's slot in one chunk: its entry count, first kDecR*512 entries and
+// (bitmap format) the thread's bitmap word, all loaded with one round of independent loads.
+struct DecItem {
+  uint32_t id[kDecR];
+  float v[kDecR];
+  uint32_t bw, cnt;
+};
+
+// LDS-read values are VGPRs to the compiler; the meta record is wave-uniform, so move it to
+// SGPRs (scalar base + 32-bit lane offset addressing, no 64-bit VGPR address per load).
+__device__ __forceinline__ uint32_t uni32(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)x);
+}
+__device__ __forceinline__ uint64_t uni64(uint64_t x) {
+  return ((uint64_t)uni32((uint32_t)(x >> 32)) << 32) | uni32((uint32_t)x);
+}
+template <typename T>
+__device__ __forceinline__ T* uni_ptr(T* p) { return (T*)uni64((uint64_t)p); }
+
+__device__ __forceinline__ DecMeta uni_meta(const DecMeta& m) {
+  DecMeta u;
+  u.idx = uni_ptr(m.idx); u.val = uni_ptr(m.val); u.cnt = uni_ptr(m.cnt);
+  u.seed = uni64(m.seed); u.offset = uni64(m.offset);
+  u.p = __longlong_as_double((long long)uni64((uint64_t)__double_as_longlong(m.p)));
+  u.thresh = uni64(m.thresh); u.w = __uint_as_float(uni32(__float_as_uint(m.w)));
+  u.flags = uni32(m.flags);
+  return u;
+}
+
+// Unconditional loads (inside the chunk's 8192-entry slot; entries past cnt are ignored):
+// no divergent branch around them, so the compiler waits on exactly one ring slot
+// (vmcnt(N)) while the other kDecDepth-1 items stay in flight.
+template <int FMT>
+__device__ __forceinline__ void dec_load(DecItem& it, const DecMeta& pm, uint32_t c, int tid) {
+  const uint64_t lo = (uint64_t)c * kChunk;
+  gf32* val = (gf32*)pm.val + lo;                 // chunk slot base (scalar)
+  gu32* idx = (gu32*)pm.idx + lo;
+  it.cnt = ((gu32*)pm.cnt)[c];
+#pragma unroll
+  for (int r = 0; r < kDecR; ++r) {
+    const uint32_t e = (uint32_t)(tid + r * kDBlock);
+    it.v[r] = val[e];
+    if (FMT == FC_FMT_IDXVAL) it.id[r] = idx[e];
+  }
+  if (FMT == FC_FMT_BITMAP) it.bw = ((gu32*)pm.idx + (uint64_t)c * kChunkWords)[tid];
+}
+
+__device__ __forceinline__ PktCache meta_pkt(const DecMeta& pm) {
+  PktCache c;
+  c.idx = pm.idx; c.val = pm.val; c.bitmap = pm.idx; c.cnt = pm.cnt; c.w = pm.w;
+  c.thresh = pm.thresh;
+  c.ib = pm.flags & 0xffu; c.codec = (pm.flags >> 8) & 0xffu; c.key_mode = pm.flags >> 16;
+  c.seed = pm.seed; c.offset = pm.offset; c.p = pm.p;
+  return c;
+}
+
+// Persistent, software-pipelined decode.  Workgroup b owns chunks b, b + G, ...; for every
+// chunk it walks the packets in G's row order (gar.py:44), one "item" (packet, chunk) at a
+// time.  Items are taken kDecGroup at a time: the group's loads (entry count, first 1024
+// entries, bitmap word) are issued together in straight-line code, then the items are
+// expanded one by one, each waiting only for its own loads (exact vmcnt; a loop-carried
+// register ring made the compiler fall back to near-vmcnt(0) waits).  Four resident
+// workgroups per CU overlap one group's latency with the others' work.
+// Per item: scatter into the LDS tile (+ presence bits), barrier, every lane folds its 32
+// elements, barrier.
 template <int FMT, bool ACC, bool OUT64>
-__global__ __launch_bounds__(kBlock) void k_decode(DecodeArgs a) {
-  __shared__ __attribute__((aligned(16))) float tile[FMT == FC_FMT_IDXVAL ? kChunk : 4];
-  __shared__ uint32_t bits[kChunkWords];
+__global__ __launch_bounds__(kDBlock, kDecBlocksPerCU) void k_decode(DecodeArgs a) {
+  __shared__ __attribute__((aligned(16))) float tile[kChunk];   // IDXVAL scatter / BITMAP values
+  __shared__ uint32_t bits[2][kChunkWords];                      // presence (double-buffered)
   __shared__ uint32_t wpre[kChunkWords];
+  __shared__ DecMeta s_meta[ACC ? kDecMaxM : 1];
   __shared__ uint32_t s_tmp[8];
   const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
-  const uint32_t c = blockIdx.x;
-  const uint64_t base = (uint64_t)c * kChunk;
+  const uint32_t M = ACC ? (uint32_t)a.m : 1u;
+  const uint32_t nch = (uint32_t)((a.n + kChunk - 1) / kChunk);
+  const uint32_t G = gridDim.x;
+  if (blockIdx.x >= nch) return;
+  const uint32_t J = (nch - blockIdx.x + G - 1) / G;             // chunks of this workgroup
+  const uint32_t T = J * M;                                      // items
 
-  float4 acc[kVec];
-  double4 out64[OUT64 ? kVec : 1];
-  (void)out64;
-
-  for (int m = 0; m < a.m; ++m) {
-    const PktCache pk = load_pkt(ACC ? a.views[m] : a.one);
-    const uint32_t lo = c * (uint32_t)kChunk, hi = lo + pk.cnt[c];   // chunk c's slot
-    __syncthreads();                                     // previous packet fully consumed
-    if (FMT == FC_FMT_IDXVAL) {
-      bits[tid] = 0;
-      __syncthreads();
-      for (uint32_t e = lo + tid; e < hi; e += kBlock) {
-        const uint32_t id = pk.idx[e];
-        const float v = pk.val[e];
-        const uint32_t loc = id - (uint32_t)base;
-        if (loc < (uint32_t)kChunk && entry_kept(pk, id, v)) {
-          tile[loc] = v;
-          atomicOr(&bits[loc >> 5], 1u << (loc & 31));
-        }
-      }
-    } else {
-      const uint32_t wd = pk.bitmap[(uint64_t)c * kChunkWords + tid];
-      bits[tid] = wd;
-      wpre[tid] = block_excl_scan(__popc(wd), s_tmp, nullptr);
-    }
-    __syncthreads();
-    const float dz = dropped_f32(pk);
-#pragma unroll
-    for (int i = 0; i < kVec; ++i) {
-      const uint32_t loc0 = (uint32_t)(i * 1024 + w * 256 + lane * 4);
-      const uint32_t q = loc0 >> 5, sh = loc0 & 31;
-      const uint32_t wq = bits[q];
-      const uint32_t nib = (wq >> sh) & 0xfu;
-      float4 d;
-      if (FMT == FC_FMT_IDXVAL) {
-        const float4 t = *reinterpret_cast<const float4*>(&tile[loc0]);
-        d.x = (nib & 1u) ? kept_f32(t.x, pk) : dz;
-        d.y = (nib & 2u) ? kept_f32(t.y, pk) : dz;
-        d.z = (nib & 4u) ? kept_f32(t.z, pk) : dz;
-        d.w = (nib & 8u) ? kept_f32(t.w, pk) : dz;
-        if (OUT64) {
-          out64[i].x = (nib & 1u) ? kept_f64(t.x, pk) : (double)dz;
-          out64[i].y = (nib & 2u) ? kept_f64(t.y, pk) : (double)dz;
-          out64[i].z = (nib & 4u) ? kept_f64(t.z, pk) : (double)dz;
-          out64[i].w = (nib & 8u) ? kept_f64(t.w, pk) : (double)dz;
-        }
-      } else {
-        uint32_t r = lo + wpre[q] + __popc(wq & ((1u << sh) - 1u));
-        float raw[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) raw[j] = ((nib >> j) & 1u) ? pk.val[r + __popc(nib & ((1u << j) - 1u))] : 0.f;
-        d.x = (nib & 1u) ? kept_f32(raw[0], pk) : dz;
-        d.y = (nib & 2u) ? kept_f32(raw[1], pk) : dz;
-        d.z = (nib & 4u) ? kept_f32(raw[2], pk) : dz;
-        d.w = (nib & 8u) ? kept_f32(raw[3], pk) : dz;
-        if (OUT64) {
-          out64[i].x = (nib & 1u) ? kept_f64(raw[0], pk) : (double)dz;
-          out64[i].y = (nib & 2u) ? kept_f64(raw[1], pk) : (double)dz;
-          out64[i].z = (nib & 4u) ? kept_f64(raw[2], pk) : (double)dz;
-          out64[i].w = (nib & 8u) ? kept_f64(raw[3], pk) : (double)dz;
-        }
-      }
-      if (ACC) {
-        const float4 cw = make_float4(__fmul_rn(d.x, pk.w), __fmul_rn(d.y, pk.w),
-                                      __fmul_rn(d.z, pk.w), __fmul_rn(d.w, pk.w));
-        if (m == 0) acc[i] = cw;
-        else acc[i] = make_float4(__fadd_rn(acc[i].x, cw.x), __fadd_rn(acc[i].y, cw.y),
-                                  __fadd_rn(acc[i].z, cw.z), __fadd_rn(acc[i].w, cw.w));
-      } else {
-        acc[i] = d;
-      }
-    }
+  if (tid < (int)M) {
+    const fc_packet_view v = ACC ? a.views[tid] : a.one;
+    const fc_packet_hdr* h = v.hdr;
+    DecMeta d;
+    d.idx = FMT == FC_FMT_IDXVAL ? v.idx : v.bitmap; d.val = v.val; d.cnt = v.cnt;
+    d.seed = h->seed; d.offset = h->offset; d.p = h->p;
+    d.thresh = h->thresh; d.w = v.weight;
+    d.flags = (h->index_bits & 0xffu) | ((h->codec & 0xffu) << 8) | (h->key_mode << 16);
+    s_meta[tid] = d;
   }
+  bits[0][tid] = 0; bits[1][tid] = 0;
+  __syncthreads();
+
+  float4 acc[ACC ? kDVec : 1];
+  uint32_t lj = 0, lm = 0;                                       // load cursor (item -> j, m)
+  uint32_t pj = 0, pm_i = 0;                                     // process cursor
+  for (uint32_t t0 = 0; t0 < T; t0 += kDecGroup) {
+    DecItem grp[kDecGroup];
 #pragma unroll
-  for (int i = 0; i < kVec; ++i) {
-    const uint64_t e = base + (uint64_t)(i * 1024 + w * 256 + lane * 4);
-    if (OUT64) {
-      double* o = reinterpret_cast<double*>(a.out);
-      if (e + 0 < a.n) o[e + 0] = out64[i].x;
-      if (e + 1 < a.n) o[e + 1] = out64[i].y;
-      if (e + 2 < a.n) o[e + 2] = out64[i].z;
-      if (e + 3 < a.n) o[e + 3] = out64[i].w;
-    } else {
-      store_out(reinterpret_cast<float*>(a.out), e, a.n, acc[i]);
+    for (int d = 0; d < kDecGroup; ++d) {                        // past the end: re-load (ignored)
+      const uint32_t c = blockIdx.x + min(lj, J - 1) * G;
+      dec_load<FMT>(grp[d], uni_meta(s_meta[lm]), c, tid);
+      if (++lm == M) { lm = 0; ++lj; }
+    }
+#pragma unroll
+    for (int d = 0; d < kDecGroup; ++d) {
+      const uint32_t t = t0 + d;
+      if (t < T) {                                               // uniform
+        const DecItem& cur = grp[d];
+        const uint32_t c = blockIdx.x + pj * G;
+        const uint64_t base = (uint64_t)c * kChunk;
+        const uint32_t m = pm_i;
+        const DecMeta pm = uni_meta(s_meta[m]);
+        const PktCache pk = meta_pkt(pm);
+        const uint32_t cntv = uni32(cur.cnt);
+        uint32_t* bb = bits[t & 1];
+        if (ACC && m == 0 && a.acc_in) {
+#pragma unroll
+          for (int i = 0; i < kDVec; ++i)
+            acc[i] = load4(reinterpret_cast<const float*>(a.out),
+                           base + (uint32_t)(i * 1024 + w * 256 + lane * 4), a.n);
+        }
+        // ---- expand into LDS ----------------------------------------------------------------
+        if (FMT == FC_FMT_IDXVAL) {
+          // fp32 outputs get fl32(fl64(g)/p) (compression.py:60) once per entry, here
+          const bool scale = !OUT64 && pk.codec == FC_CODEC_DROPOUT_UNBIASED;   // uniform
+          if ((pk.key_mode == FC_KEY_PHILOX && pk.thresh != 0) || scale) {
+            for (int r = 0; r < kDecR; ++r) {          // rand-k slack filter / scaling: one
+              const uint32_t e = (uint32_t)(tid + r * kDBlock);   // entry at a time (VGPRs)
+              const uint32_t loc = cur.id[r] - (uint32_t)base;
+              if (e < cntv && loc < (uint32_t)kChunk && entry_kept(pk, cur.id[r], cur.v[r])) {
+                tile[loc] = scale ? (float)((double)cur.v[r] / pk.p) : cur.v[r];
+                atomicOr(&bb[loc >> 5], 1u << (loc & 31));
+              }
+            }
+          } else {
+#pragma unroll
+            for (int r = 0; r < kDecR; ++r) {
+              const uint32_t e = (uint32_t)(tid + r * kDBlock);
+              const uint32_t loc = cur.id[r] - (uint32_t)base;
+              const bool keep = pk.thresh == 0 ||
+                                comp_of(mag_key(cur.v[r]), cur.id[r], pk.ib) >= pk.thresh;
+              if (e < cntv && loc < (uint32_t)kChunk && keep) {
+                tile[loc] = cur.v[r];
+                atomicOr(&bb[loc >> 5], 1u << (loc & 31));
+              }
+            }
+          }
+          if (cntv > (uint32_t)(kDecR * kDBlock)) {              // dense slot (uniform, rare)
+            gf32* pval = (gf32*)pm.val + base;
+            gu32* pidx = (gu32*)pm.idx + base;
+            for (uint32_t e = (uint32_t)(kDecR * kDBlock + tid); e < cntv; e += kDBlock) {
+              const uint32_t id = pidx[e];
+              const float v = pval[e];
+              const uint32_t loc = id - (uint32_t)base;
+              if (loc < (uint32_t)kChunk && entry_kept(pk, id, v)) {
+                tile[loc] = scale ? (float)((double)v / pk.p) : v;
+                atomicOr(&bb[loc >> 5], 1u << (loc & 31));
+              }
+            }
+            __builtin_amdgcn_s_waitcnt(0x0F70);                  // vmcnt(0): none left pending
+          }
+        } else {
+          bb[tid] = cur.bw;
+          const bool scale = !OUT64 && pk.codec == FC_CODEC_DROPOUT_UNBIASED;   // uniform
+          if (scale) {
+#pragma unroll
+            for (int r = 0; r < kDecR; ++r) {
+              const uint32_t e = (uint32_t)(tid + r * kDBlock);
+              if (e < cntv) tile[e] = (float)((double)cur.v[r] / pk.p);  // compression.py:60
+            }
+          } else {
+#pragma unroll
+            for (int r = 0; r < kDecR; ++r) {
+              const uint32_t e = (uint32_t)(tid + r * kDBlock);
+              if (e < cntv) tile[e] = cur.v[r];
+            }
+          }
+          if (cntv > (uint32_t)(kDecR * kDBlock)) {
+            gf32* pval = (gf32*)pm.val + base;
+            for (uint32_t e = (uint32_t)(kDecR * kDBlock + tid); e < cntv; e += kDBlock)
+              tile[e] = scale ? (float)((double)pval[e] / pk.p) : pval[e];
+            __builtin_amdgcn_s_waitcnt(0x0F70);                  // vmcnt(0)
+          }
+          wpre[tid] = block_excl_scan(__popc(cur.bw), s_tmp, nullptr);
+        }
+        __syncthreads();
+        // ---- every lane folds its own 32 elements ------------------------------------------
+        const float dz = dropped_f32(pk);
+        const bool unb = pk.codec == FC_CODEC_DROPOUT_UNBIASED;
+#pragma unroll
+        for (int i = 0; i < kDVec; ++i) {
+          const uint32_t loc0 = (uint32_t)(i * 1024 + w * 256 + lane * 4);
+          const uint32_t q = loc0 >> 5, sh = loc0 & 31;
+          const uint32_t wq = bb[q];
+          const uint32_t nib = (wq >> sh) & 0xfu;
+          float raw[4];
+          if (FMT == FC_FMT_IDXVAL) {
+            const float4 tv = *reinterpret_cast<const float4*>(&tile[loc0]);
+            raw[0] = tv.x; raw[1] = tv.y; raw[2] = tv.z; raw[3] = tv.w;
+          } else {
+            const uint32_t r0 = wpre[q] + __popc(wq & ((1u << sh) - 1u));
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj)
+              raw[jj] = ((nib >> jj) & 1u) ? tile[r0 + __popc(nib & ((1u << jj) - 1u))] : 0.f;
+          }
+          const uint64_t eo = base + loc0;
+          if (OUT64) {   // fp64 result (dropout, compression.py:52/60): divide here, per element
+            double* o = reinterpret_cast<double*>(a.out);
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj)
+              if (eo + jj < a.n)
+                o[eo + jj] = ((nib >> jj) & 1u) ? (unb ? (double)raw[jj] / pk.p : (double)raw[jj])
+                                                : (double)dz;
+            continue;
+          }
+          // fp32 paths: the tile already holds the kept value (fl32(fl64(g)/p) applied once
+          // per entry at scatter time, not per element here)
+          const float4 dv = make_float4((nib & 1u) ? raw[0] : dz, (nib & 2u) ? raw[1] : dz,
+                                        (nib & 4u) ? raw[2] : dz, (nib & 8u) ? raw[3] : dz);
+          if (ACC) {
+            const float4 cw = make_float4(__fmul_rn(dv.x, pk.w), __fmul_rn(dv.y, pk.w),
+                                          __fmul_rn(dv.z, pk.w), __fmul_rn(dv.w, pk.w));
+            if (m == 0 && !a.acc_in) acc[i] = cw;
+            else acc[i] = make_float4(__fadd_rn(acc[i].x, cw.x), __fadd_rn(acc[i].y, cw.y),
+                                      __fadd_rn(acc[i].z, cw.z), __fadd_rn(acc[i].w, cw.w));
+          } else {
+            store_out(reinterpret_cast<float*>(a.out), eo, a.n, dv);   // single packet: done
+          }
+        }
+        __syncthreads();                                         // tile / wpre free again
+        if (FMT == FC_FMT_IDXVAL) bb[tid] = 0;                   // for item t + 2
+        if (ACC && m + 1 == M) {                                 // chunk done: write the sum
+#pragma unroll
+          for (int i = 0; i < kDVec; ++i)
+            store_out(reinterpret_cast<float*>(a.out),
+                      base + (uint64_t)(i * 1024 + w * 256 + lane * 4), a.n, acc[i]);
+        }
+        if (++pm_i == M) { pm_i = 0; ++pj; }
+      }
     }
   }
 }

@@ -88,6 +88,8 @@ __device__ void bitonic_desc(uint64_t* sv, uint32_t P2) {
 // Sampling: level 1 (key >> 19, 4096 bins) and level 2 ((key >> 7) & 0xfff inside the two
 // level-1 bins that hold the bracket ranks).  Payload = global atomics only.
 // --------------------------------------------------------------------------------------
+constexpr int kSampleSegs = 4;   // segments per workgroup (grid = ceil(nseg / 4))
+
 template <int KM, int LEVEL>
 __global__ __launch_bounds__(kBlock) void k_sample(const float* __restrict__ g, SamplePlan P,
                                                    uint64_t seed, uint64_t off, WsPtrs W,
@@ -103,13 +105,26 @@ __global__ __launch_bounds__(kBlock) void k_sample(const float* __restrict__ g, 
   uint32_t b1_hi = 0, b1_lo = 0, hi_none = 0, lo_all = 0;
   if (LEVEL == 2) { b1_hi = S->b1_hi; b1_lo = S->b1_lo; hi_none = S->hi_none; lo_all = S->lo_all; }
   __syncthreads();
-  for (uint32_t s = blockIdx.x; s < P.nseg; s += gridDim.x) {
-    const uint64_t st = seg_start(P, s);
-    const uint64_t lim = P.full ? (st + 1024 < P.n ? st + 1024 : P.n) : st + 1024;
-    const uint64_t e = st + (uint64_t)tid * 4;
+  // all of this workgroup's segments loaded up front (one memory latency, not kSampleSegs)
+  float4 xs[kSampleSegs];
+  uint64_t es[kSampleSegs], lims[kSampleSegs];
+#pragma unroll
+  for (int q = 0; q < kSampleSegs; ++q) {
+    const uint32_t s = blockIdx.x + (uint32_t)q * gridDim.x;
+    es[q] = lims[q] = 0;
+    xs[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (s < P.nseg) {
+      const uint64_t st = seg_start(P, s);
+      lims[q] = P.full ? (st + 1024 < P.n ? st + 1024 : P.n) : st + 1024;
+      es[q] = st + (uint64_t)tid * 4;
+      if (es[q] < lims[q]) xs[q] = load4(g, es[q], lims[q]);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < kSampleSegs; ++q) {
+    const uint64_t e = es[q], lim = lims[q];
     if (e < lim) {
-      const float4 x = load4(g, e, lim);
-      const uint4 kk = keys4<KM>(x, e, seed, off);
+      const uint4 kk = keys4<KM>(xs[q], e, seed, off);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         if (e + j >= lim) break;
@@ -171,12 +186,21 @@ __global__ __launch_bounds__(kBlock) void k_sample(const float* __restrict__ g, 
 
 
 // --------------------------------------------------------------------------------------
-// k_compact: one independent workgroup per 8192-element chunk (slotted packet, no global
-// scan).  Element layout: e = i*1024 + w*256 + lane*4 + j (i < 8, w < 4, j < 4): each wave
-// instruction moves 1 KiB contiguous and (i, w, lane, j) order is ascending index order, so
-// ballot + mbcnt + a 32-slot LDS scan give ordered offsets inside the chunk's slot.
+// k_compact: one independent 512-thread workgroup per 8192-element chunk (slotted packet,
+// no global scan).  Element layout: e = i*2048 + w*256 + lane*4 + j (i < 4, w < 8, j < 4):
+// each wave instruction moves 1 KiB contiguous and (i, w, lane, j) order is ascending index
+// order, so ballot + mbcnt + a 32-slot LDS scan give ordered offsets inside the chunk's slot.
+// Listed entries are staged in LDS and leave as coalesced 16-B stores; candidate histogram
+// bins are flushed 64 lanes per atomic instruction.
 // --------------------------------------------------------------------------------------
 enum Pred : int { kPredKey = 0, kPredMask = 1, kPredBern = 2 };
+
+constexpr int kCBlock = 512;
+constexpr int kCWaves = kCBlock / 64;            // 8
+constexpr int kCVec = kChunk / (kCBlock * 4);    // 4 float4 per thread
+constexpr int kCSlots = kCVec * kCWaves;         // 32
+constexpr int kStage = 2048;                     // LDS-staged entries per chunk
+static_assert(kCSlots == 32, "slot scan assumes 32 slots");
 
 struct CompactArgs {
   const float* g;
@@ -196,93 +220,140 @@ struct CompactArgs {
   HdrInit HI;
 };
 
+// Stage the listed elements of one float4 (bits 0..3 of `bb`) at LDS positions pos, pos+1..
+// as packed {chunk-local index, value bits}.  LDS store cost is per wave instruction, not per
+// active lane: instead of one store per element, run only as many rounds as the busiest lane
+// of the wave has listed elements (~2 at f = 0.1), one b64 store per round.  Lanes with
+// nothing left write their private dummy slot kStage + lane (branchless, conflict-free).
+template <int PRED>
+__device__ __forceinline__ void stage_f4(uint2* st, float4 v4, uint32_t bb, uint32_t nanb,
+                                         uint32_t pos, uint32_t l0, int lane) {
+  bb &= 0xfu;
+  while (__any(bb != 0u)) {
+    const bool sel = bb != 0u;
+    const uint32_t j = (uint32_t)__builtin_ctz(bb | 0x10u);
+    float v = j == 0 ? v4.x : j == 1 ? v4.y : j == 2 ? v4.z : v4.w;
+    if (PRED != kPredKey) v = ((nanb >> j) & 1u) ? __uint_as_float(0x7fc00000u) : v;
+    st[sel ? pos : (uint32_t)kStage + lane] = make_uint2(l0 + j, __float_as_uint(v));
+    pos += sel;
+    bb &= bb - 1u;
+  }
+}
+
+#ifndef FC_COMPACT_WAVES_PER_EU
+#define FC_COMPACT_WAVES_PER_EU 6
+#endif
 template <int KM, int PRED, int FMT>
-__global__ __launch_bounds__(kBlock) void k_compact(CompactArgs a) {
-  __shared__ uint32_t s_ent[kSlots], s_cnd[kSlots];
+__global__ __launch_bounds__(kCBlock, FC_COMPACT_WAVES_PER_EU) void k_compact(CompactArgs a) {
+  __shared__ uint32_t s_ent[kCSlots], s_cnd[kCSlots], s_tot[2];
+  // staging: one packed {chunk-local index, value bits} per listed element; lanes with
+  // nothing left to write in a round store to their own dummy slot kStage + lane (one shared
+  // dummy made every store a ~58-way LDS bank conflict — measured 65 us of a 165 us launch)
+  __shared__ __attribute__((aligned(16))) uint2 st[kStage + 64];
+  __shared__ uint16_t s_cbin[PRED == kPredKey ? kStage + 2 : 2];
   const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
   TopkState* S = a.W.st;
   const uint32_t chunk = blockIdx.x;
-  const uint64_t base = (uint64_t)chunk * kChunk;
+  const uint32_t base = chunk * (uint32_t)kChunk;          // n < 2^32
+  const uint32_t n32 = (uint32_t)a.n;
   if (a.write_hdr && chunk == 0 && tid == 0) write_hdr_static(a.hdr, a.HI);  // sole writer
 
-  uint64_t L64 = 0;
-  uint32_t t_lo = 0, t_hi = 0xffffffffu, cand_on = 0, sbin = 0;
+  uint32_t Lk = 0;   // key part of L64; 0xffffffff (above every key) selects nothing
+  uint32_t Li = 0, t_lo = 0, t_hi = 0xffffffffu, cand_on = 0, sbin = 0;
   if (PRED == kPredKey) {
-    L64 = S->L64; t_lo = S->t_lo; t_hi = S->t_hi; cand_on = S->cand_on; sbin = S->sbin;
+    const uint64_t L64 = S->L64;
+    const bool none = L64 == kSelectNothing;
+    Lk = none ? 0xffffffffu : (uint32_t)(L64 >> a.ib);
+    Li = none ? 0xffffffffu : (uint32_t)(L64 & ((1ull << a.ib) - 1));
+    t_lo = S->t_lo; t_hi = S->t_hi; cand_on = S->cand_on; sbin = S->sbin;
   }
 
-  float4 x[kVec];
+  float4 x[kCVec];
 #pragma unroll
-  for (int i = 0; i < kVec; ++i)
-    x[i] = load4(a.g, base + (uint64_t)(i * 1024 + w * 256 + lane * 4), a.n);
+  for (int i = 0; i < kCVec; ++i)
+    x[i] = load4(a.g, (uint64_t)base + (uint32_t)(i * 2048 + w * 256 + lane * 4), a.n);
 
-  uint32_t pbits = 0, cbits = 0;   // bit (i*4 + j): listed / candidate (or NaN stand-in)
+  // ---- predicates (branchless): bit (i*4 + j) -------------------------------------------
+  uint32_t pbits = 0, cbits = 0;   // listed / candidate (or NaN stand-in for mask codecs)
 #pragma unroll
-  for (int i = 0; i < kVec; ++i) {
-    const uint64_t e0 = base + (uint64_t)(i * 1024 + w * 256 + lane * 4);
+  for (int i = 0; i < kCVec; ++i) {
+    const uint32_t e0 = base + (uint32_t)(i * 2048 + w * 256 + lane * 4);
     uint4 kk = make_uint4(0, 0, 0, 0);
     if (PRED == kPredKey) kk = keys4<KM>(x[i], e0, a.seed, a.offset);
     if (PRED == kPredBern) kk = philox_block(e0 >> 2, a.seed, a.offset);
     uint32_t mword = 0;
-    if (PRED == kPredMask && e0 < a.n) mword = a.mask[e0 >> 5] >> (e0 & 31);
+    if (PRED == kPredMask && e0 < n32) mword = a.mask[e0 >> 5] >> (e0 & 31);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const uint64_t e = e0 + j;
-      const bool valid = e < a.n;
-      bool p;
+      const uint32_t e = e0 + j;
+      const bool valid = e < n32;
+      bool p, c;
       if (PRED == kPredKey) {
         const uint32_t key = u4get(kk, j);
-        p = valid && comp_of(key, (uint32_t)e, a.ib) >= L64;
-        if (valid && cand_on && key >= t_lo && key <= t_hi) {
-          cbits |= 1u << (i * 4 + j);
-          atomicAdd(&a.W.chist[(key - t_lo) >> sbin], 1u);
-        }
+        p = valid & ((key > Lk) | ((key == Lk) & (e >= Li)));          // branchless
+        c = valid & (cand_on != 0) & (key >= t_lo) & (key <= t_hi);
       } else {
         const bool keep = PRED == kPredMask ? ((mword >> j) & 1u) != 0
                                             : (uint64_t)u4get(kk, j) < a.bern_thr;
         const uint32_t ab = __float_as_uint(f4get(x[i], j)) & 0x7fffffffu;
-        const bool nan_standin = a.nonfinite_keep && !keep && ab >= 0x7f800000u;  // g*0 = NaN
-        p = valid && (keep || nan_standin);
-        if (valid && nan_standin) cbits |= 1u << (i * 4 + j);
+        c = a.nonfinite_keep && !keep && ab >= 0x7f800000u;    // g*0 = NaN stand-in
+        p = valid && (keep || c);
+        c = c && valid;
       }
-      if (p) pbits |= 1u << (i * 4 + j);
+      pbits |= (uint32_t)p << (i * 4 + j);
+      cbits |= (uint32_t)c << (i * 4 + j);
     }
   }
 
-  // per-(i, w) counts (+ bitmap words, natural bit order)
+  // ---- ordered offsets: per-i lane counts packed 2 x 16 bit, one DPP scan per pair ----------
+  const uint32_t c01 = __popc(pbits & 0xfu) | (__popc((pbits >> 4) & 0xfu) << 16);
+  const uint32_t c23 = __popc((pbits >> 8) & 0xfu) | (__popc((pbits >> 12) & 0xfu) << 16);
+  const uint32_t i01 = wave_incl_scan(c01), i23 = wave_incl_scan(c23);
+  const uint32_t x01 = i01 - c01, x23 = i23 - c23;         // exclusive (no field borrow)
+  if (lane == 63) {
+    s_ent[0 * kCWaves + w] = i01 & 0xffffu; s_ent[1 * kCWaves + w] = i01 >> 16;
+    s_ent[2 * kCWaves + w] = i23 & 0xffffu; s_ent[3 * kCWaves + w] = i23 >> 16;
+  }
+  const bool wave_cand = PRED == kPredKey && __any(cbits != 0);
+  uint32_t xc01 = 0, xc23 = 0;
+  if (PRED == kPredKey) {
+    if (wave_cand) {
+      const uint32_t d01 = __popc(cbits & 0xfu) | (__popc((cbits >> 4) & 0xfu) << 16);
+      const uint32_t d23 = __popc((cbits >> 8) & 0xfu) | (__popc((cbits >> 12) & 0xfu) << 16);
+      const uint32_t j01 = wave_incl_scan(d01), j23 = wave_incl_scan(d23);
+      xc01 = j01 - d01; xc23 = j23 - d23;
+      if (lane == 63) {
+        s_cnd[0 * kCWaves + w] = j01 & 0xffffu; s_cnd[1 * kCWaves + w] = j01 >> 16;
+        s_cnd[2 * kCWaves + w] = j23 & 0xffffu; s_cnd[3 * kCWaves + w] = j23 >> 16;
+      }
+    } else if (lane == 0) {
+      s_cnd[0 * kCWaves + w] = 0; s_cnd[1 * kCWaves + w] = 0;
+      s_cnd[2 * kCWaves + w] = 0; s_cnd[3 * kCWaves + w] = 0;
+    }
+  }
+  if (FMT == FC_FMT_BITMAP) {   // bitmap words (natural bit order) from 4 ballots per i
 #pragma unroll
-  for (int i = 0; i < kVec; ++i) {
-    const uint64_t m0 = __ballot((pbits >> (i * 4 + 0)) & 1u);
-    const uint64_t m1 = __ballot((pbits >> (i * 4 + 1)) & 1u);
-    const uint64_t m2 = __ballot((pbits >> (i * 4 + 2)) & 1u);
-    const uint64_t m3 = __ballot((pbits >> (i * 4 + 3)) & 1u);
-    uint32_t nc = 0;
-    if (PRED == kPredKey) {
-      nc = __popcll(__ballot((cbits >> (i * 4 + 0)) & 1u)) + __popcll(__ballot((cbits >> (i * 4 + 1)) & 1u)) +
-           __popcll(__ballot((cbits >> (i * 4 + 2)) & 1u)) + __popcll(__ballot((cbits >> (i * 4 + 3)) & 1u));
-    }
-    if (lane == 0) {
-      s_ent[i * kWaves + w] = __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3);
-      s_cnd[i * kWaves + w] = nc;
-    }
-    if (FMT == FC_FMT_BITMAP && lane < 8) {
-      const int sh = lane * 8;
-      const uint32_t word = spread4((uint32_t)(m0 >> sh)) | (spread4((uint32_t)(m1 >> sh)) << 1) |
-                            (spread4((uint32_t)(m2 >> sh)) << 2) | (spread4((uint32_t)(m3 >> sh)) << 3);
-      a.bitmap[(base + (uint64_t)(i * 1024 + w * 256)) / 32 + lane] = word;
+    for (int i = 0; i < kCVec; ++i) {
+      const uint64_t m0 = __ballot((pbits >> (i * 4 + 0)) & 1u);
+      const uint64_t m1 = __ballot((pbits >> (i * 4 + 1)) & 1u);
+      const uint64_t m2 = __ballot((pbits >> (i * 4 + 2)) & 1u);
+      const uint64_t m3 = __ballot((pbits >> (i * 4 + 3)) & 1u);
+      if (lane < 8) {
+        const int sh = lane * 8;
+        const uint32_t word = spread4((uint32_t)(m0 >> sh)) | (spread4((uint32_t)(m1 >> sh)) << 1) |
+                              (spread4((uint32_t)(m2 >> sh)) << 2) | (spread4((uint32_t)(m3 >> sh)) << 3);
+        a.bitmap[(base + (uint32_t)(i * 2048 + w * 256)) / 32 + lane] = word;
+      }
     }
   }
   __syncthreads();
-  if (w == 0) {   // exclusive scan of the 32 slots (lanes 0..31) for both counts
-    const uint32_t ve = lane < kSlots ? s_ent[lane] : 0u, vc = lane < kSlots ? s_cnd[lane] : 0u;
-    uint32_t ie = ve, ic = vc;
-#pragma unroll
-    for (int o = 1; o < 32; o <<= 1) {
-      const uint32_t te = __shfl_up(ie, o, 64), tc = __shfl_up(ic, o, 64);
-      if (lane >= o) { ie += te; ic += tc; }
-    }
-    if (lane < kSlots) { s_ent[lane] = ie - ve; s_cnd[lane] = ic - vc; }
-    if (lane == kSlots - 1) {
+  if (w == 0) {   // exclusive scan of the 32 (i, w) slots (lanes 0..31) for both counts
+    const uint32_t ve = lane < kCSlots ? s_ent[lane] : 0u, vc = lane < kCSlots ? s_cnd[lane] : 0u;
+    const uint32_t ie = wave_incl_scan(ve);
+    const uint32_t ic = PRED == kPredKey ? wave_incl_scan(vc) : 0u;
+    if (lane < kCSlots) { s_ent[lane] = ie - ve; if (PRED == kPredKey) s_cnd[lane] = ic - vc; }
+    if (lane == kCSlots - 1) {
+      s_tot[0] = ie; s_tot[1] = ic;
       a.cnt[chunk] = ie;
       if (PRED == kPredKey) {
         a.W.ccnt[chunk] = ic;
@@ -293,42 +364,90 @@ __global__ __launch_bounds__(kBlock) void k_compact(CompactArgs a) {
   }
   __syncthreads();
 
+  const uint32_t tot_e = s_tot[0];
   const uint64_t slot = base;                     // entries slot of this chunk
-  const uint64_t cslot = (uint64_t)chunk * kCandSlot;
+#ifdef FC_ABLATE
+  asm volatile("" ::"v"(pbits), "v"(cbits), "v"(x01), "v"(x23));   // diagnostic build only
+  if (FC_ABLATE == 1) return;
+#endif
+#ifdef FC_ABLATE
+  constexpr bool kAblCand = FC_ABLATE == 2, kAblCopy = FC_ABLATE == 3, kAblStage = FC_ABLATE == 4;
+#else
+  constexpr bool kAblCand = false, kAblCopy = false, kAblStage = false;
+#endif
+  if (tot_e <= (uint32_t)kStage && !kAblStage) {  // block-uniform: stage in LDS
+    // LDS store cost is per wave instruction, not per active lane: instead of one store per
+    // element (32 per thread, ~1 GB of LDS traffic per 128M launch) each float4 runs only as
+    // many rounds as its busiest lane has listed elements (~2 at f = 0.1), one b64 per round.
+    stage_f4<PRED>(st, x[0], pbits, cbits, s_ent[0 * kCWaves + w] + (x01 & 0xffffu), 0 * 2048 + w * 256 + lane * 4, lane);
+    stage_f4<PRED>(st, x[1], pbits >> 4, cbits >> 4, s_ent[1 * kCWaves + w] + (x01 >> 16), 1 * 2048 + w * 256 + lane * 4, lane);
+    stage_f4<PRED>(st, x[2], pbits >> 8, cbits >> 8, s_ent[2 * kCWaves + w] + (x23 & 0xffffu), 2 * 2048 + w * 256 + lane * 4, lane);
+    stage_f4<PRED>(st, x[3], pbits >> 12, cbits >> 12, s_ent[3 * kCWaves + w] + (x23 >> 16), 3 * 2048 + w * 256 + lane * 4, lane);
+  } else if (!kAblStage) {                        // dense chunk: direct (predicated) stores
 #pragma unroll
-  for (int i = 0; i < kVec; ++i) {
-    const uint64_t e0 = base + (uint64_t)(i * 1024 + w * 256 + lane * 4);
-    const uint32_t lo = prefix_count(__ballot((pbits >> (i * 4 + 0)) & 1u)) +
-                        prefix_count(__ballot((pbits >> (i * 4 + 1)) & 1u)) +
-                        prefix_count(__ballot((pbits >> (i * 4 + 2)) & 1u)) +
-                        prefix_count(__ballot((pbits >> (i * 4 + 3)) & 1u));
-    uint32_t pos = s_ent[i * kWaves + w] + lo;
+    for (int i = 0; i < kCVec; ++i) {
+      const uint32_t e0 = base + (uint32_t)(i * 2048 + w * 256 + lane * 4);
+      const uint32_t xi = (i & 1) ? ((i < 2 ? x01 : x23) >> 16) : ((i < 2 ? x01 : x23) & 0xffffu);
+      uint32_t pos = s_ent[i * kCWaves + w] + xi;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if ((pbits >> (i * 4 + j)) & 1u) {
-        float v = f4get(x[i], j);
-        if (PRED != kPredKey && ((cbits >> (i * 4 + j)) & 1u)) v = __uint_as_float(0x7fc00000u);
-        if (FMT == FC_FMT_IDXVAL) a.idx[slot + pos] = (uint32_t)(e0 + j);
-        a.val[slot + pos] = v;
-        ++pos;
+      for (int j = 0; j < 4; ++j) {
+        if ((pbits >> (i * 4 + j)) & 1u) {
+          float v = f4get(x[i], j);
+          if (PRED != kPredKey && ((cbits >> (i * 4 + j)) & 1u)) v = __uint_as_float(0x7fc00000u);
+          if (FMT == FC_FMT_IDXVAL) a.idx[slot + pos] = e0 + j;
+          a.val[slot + pos] = v;
+          ++pos;
+        }
       }
     }
-    if (PRED == kPredKey && cbits) {
-      const uint32_t lc = prefix_count(__ballot((cbits >> (i * 4 + 0)) & 1u)) +
-                          prefix_count(__ballot((cbits >> (i * 4 + 1)) & 1u)) +
-                          prefix_count(__ballot((cbits >> (i * 4 + 2)) & 1u)) +
-                          prefix_count(__ballot((cbits >> (i * 4 + 3)) & 1u));
-      uint32_t cpos = s_cnd[i * kWaves + w] + lc;
+  }
+  if (wave_cand && !kAblCand) {                    // candidates: rare, predicated
+    const uint64_t cslot = (uint64_t)chunk * kCandSlot;
+#pragma unroll
+    for (int i = 0; i < kCVec; ++i) {
+      if (!((cbits >> (i * 4)) & 0xfu)) continue;
+      const uint32_t e0 = base + (uint32_t)(i * 2048 + w * 256 + lane * 4);
+      const uint32_t xi = (i & 1) ? ((i < 2 ? xc01 : xc23) >> 16) : ((i < 2 ? xc01 : xc23) & 0xffffu);
+      uint32_t cpos = s_cnd[i * kCWaves + w] + xi;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         if ((cbits >> (i * 4 + j)) & 1u) {
-          const uint64_t e = e0 + j;
-          if (cpos < (uint32_t)kCandSlot)
-            a.W.cand[cslot + cpos] = comp_of(key1<KM>(f4get(x[i], j), e, a.seed, a.offset), (uint32_t)e, a.ib);
+          // recompute (2 ops) rather than keep 16 keys + indices live across the barriers
+          uint32_t e = e0 + j;
+          float xv = f4get(x[i], j);
+          asm volatile("" : "+v"(xv), "+v"(e));
+          const uint32_t key = key1<KM>(xv, e, a.seed, a.offset);
+          if (cpos < (uint32_t)kCandSlot) a.W.cand[cslot + cpos] = comp_of(key, e, a.ib);
+          const uint32_t bin = (key - t_lo) >> sbin;
+          if (cpos < (uint32_t)kStage) s_cbin[cpos] = (uint16_t)bin;
+          else atomicAdd(&a.W.chist[bin], 1u);
           ++cpos;
         }
       }
     }
+  }
+  __syncthreads();
+  if (tot_e <= (uint32_t)kStage && !kAblCopy) {   // coalesced 16-B stores of the staged slot
+    for (uint32_t t = 4 * tid; t < tot_e; t += 4 * kCBlock) {
+      if (t + 4 <= tot_e) {
+        const uint4 p0 = *reinterpret_cast<const uint4*>(&st[t]);
+        const uint4 p1 = *reinterpret_cast<const uint4*>(&st[t + 2]);
+        if (FMT == FC_FMT_IDXVAL)
+          *reinterpret_cast<uint4*>(a.idx + slot + t) =
+              make_uint4(base + p0.x, base + p0.z, base + p1.x, base + p1.z);
+        *reinterpret_cast<uint4*>(a.val + slot + t) = make_uint4(p0.y, p0.w, p1.y, p1.w);
+      } else {
+        for (uint32_t u = t; u < tot_e; ++u) {
+          if (FMT == FC_FMT_IDXVAL) a.idx[slot + u] = base + st[u].x;
+          a.val[slot + u] = __uint_as_float(st[u].y);
+        }
+      }
+    }
+  }
+  if (PRED == kPredKey) {
+    const uint32_t tot_c = s_tot[1];
+    const uint32_t nb = tot_c < (uint32_t)kStage ? tot_c : (uint32_t)kStage;
+    for (uint32_t t = tid; t < nb; t += kCBlock) atomicAdd(&a.W.chist[s_cbin[t]], 1u);
   }
 }
 
@@ -356,6 +475,7 @@ constexpr int kResolveChunksMax = 2048;   // chunks per workgroup handled throug
 __global__ __launch_bounds__(kBlock) void k_resolve(ResolveArgs a) {
   __shared__ uint64_t sv[kSmallCap];                      // 32 KiB: histogram, then sort
   __shared__ uint32_t s_pre[kResolveChunksMax + 1];       // per-chunk gather sizes (prefix)
+  __shared__ uint64_t s_ovf[kResolveChunksMax / 64];      // chunk overflowed its cand slot
   __shared__ uint32_t s_tmp[8], s_out[4], s_flag, s_cnt, s_base, s_tot[2];
   uint32_t* h = reinterpret_cast<uint32_t*>(sv);          // 4096 bins = 16 KiB
   TopkState* S = a.W.st;
@@ -393,10 +513,14 @@ __global__ __launch_bounds__(kBlock) void k_resolve(ResolveArgs a) {
     for (uint32_t b0 = 0; b0 < nc; b0 += kBlock) {
       const uint32_t c = c0 + b0 + tid;
       uint32_t sz = 0;
+      bool ovf = false;
       if (b0 + tid < nc) {
         const uint32_t cc = a.W.ccnt[c];
-        sz = cc <= (uint32_t)kCandSlot ? cc : a.cnt[c];
+        ovf = cc > (uint32_t)kCandSlot;
+        sz = ovf ? a.cnt[c] : cc;
       }
+      const uint64_t ob = __ballot(ovf);                // overflow flags, one bit per chunk
+      if ((tid & 63) == 0) s_ovf[(b0 + tid) >> 6] = ob;
       uint32_t tot;
       const uint32_t ex = block_excl_scan(sz, s_tmp, &tot);
       if (b0 + tid < nc) s_pre[b0 + tid] = carry + ex;
@@ -404,24 +528,36 @@ __global__ __launch_bounds__(kBlock) void k_resolve(ResolveArgs a) {
     }
     if (tid == 0) { s_pre[nc] = carry; s_cnt = 0; }
     __syncthreads();
-    // gather bin beta into the LDS list (sv reused after the histogram)
-    for (uint32_t j = tid; j < carry; j += kBlock) {
-      uint32_t lo = 0, hi = nc;                       // find chunk: s_pre[lo] <= j < s_pre[lo+1]
-      while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (s_pre[mid] <= j) lo = mid; else hi = mid; }
-      const uint32_t c = c0 + lo, r = j - s_pre[lo];
-      uint64_t v;
-      if (a.W.ccnt[c] <= (uint32_t)kCandSlot) {
-        v = a.W.cand[(uint64_t)c * kCandSlot + r];
-      } else {
-        const uint64_t p = (uint64_t)c * kChunk + r;
-        const uint32_t id = a.idx[p];
-        const uint32_t key = a.key_mode == FC_KEY_PHILOX ? (philox_word(id, a.seed, a.offset) >> 1)
-                                                         : mag_key(a.val[p]);
-        v = (key >= t_lo && key <= t_hi) ? comp_of(key, id, a.ib) : ~0ull;
+    // gather bin beta into the LDS list (sv reused after the histogram): kGatherU independent
+    // loads per thread in flight, then filter (one dependent global latency per round)
+    constexpr int kGatherU = 8;
+    for (uint32_t j0 = 0; j0 < carry; j0 += kBlock * kGatherU) {
+      uint64_t v[kGatherU];
+#pragma unroll
+      for (int u = 0; u < kGatherU; ++u) {
+        const uint32_t j = j0 + (uint32_t)(u * kBlock + tid);
+        v[u] = ~0ull;
+        if (j < carry) {
+          uint32_t lo = 0, hi = nc;                   // find chunk: s_pre[lo] <= j < s_pre[lo+1]
+          while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (s_pre[mid] <= j) lo = mid; else hi = mid; }
+          const uint32_t c = c0 + lo, r = j - s_pre[lo];
+          if (!((s_ovf[lo >> 6] >> (lo & 63)) & 1ull)) {
+            v[u] = a.W.cand[(uint64_t)c * kCandSlot + r];
+          } else {
+            const uint64_t p = (uint64_t)c * kChunk + r;
+            const uint32_t id = a.idx[p];
+            const uint32_t key = a.key_mode == FC_KEY_PHILOX ? (philox_word(id, a.seed, a.offset) >> 1)
+                                                             : mag_key(a.val[p]);
+            v[u] = (key >= t_lo && key <= t_hi) ? comp_of(key, id, a.ib) : ~0ull;
+          }
+        }
       }
-      if (v != ~0ull && ((((uint32_t)(v >> a.ib)) - t_lo) >> sbin) == beta) {
-        const uint32_t q = atomicAdd(&s_cnt, 1u);
-        if (q < (uint32_t)kSmallCap) sv[q] = v;
+#pragma unroll
+      for (int u = 0; u < kGatherU; ++u) {
+        if (v[u] != ~0ull && ((((uint32_t)(v[u] >> a.ib)) - t_lo) >> sbin) == beta) {
+          const uint32_t q = atomicAdd(&s_cnt, 1u);
+          if (q < (uint32_t)kSmallCap) sv[q] = v[u];
+        }
       }
     }
     __syncthreads();

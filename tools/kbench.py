@@ -1,0 +1,63 @@
+"""Kernel-level timing of one codec configuration (HIP events per kernel class).
+
+    python tools/kbench.py [--lib path/to/libfedcodec.so] [--n 134217728] [--f 0.1]
+
+Used to A/B build variants of libfedcodec.so in one process each (same device, same data).
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--lib", default=None)
+    ap.add_argument("--n", type=int, default=134_217_728)
+    ap.add_argument("--f", type=float, default=0.1)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--tag", default="")
+    ap.add_argument("--m", type=int, default=64)
+    args = ap.parse_args()
+    import torch
+    from openmsftl_amd import _lib as L
+    if args.lib:
+        L.load(os.path.abspath(args.lib))
+    from openmsftl_amd import codec
+    from openmsftl_amd.compression import kept_count
+    n, k = args.n, kept_count(args.f, args.n)
+    g = torch.randn(n, device="cuda", generator=torch.Generator(device="cuda").manual_seed(1))
+    pkt = codec.encode_top(g, k)
+    out = torch.empty_like(g)
+    for _ in range(3):
+        codec.encode_top(g, k, packet=pkt, check=False)
+        codec.decode(pkt, out=out)
+    torch.cuda.synchronize()
+    with L.KernelTimer() as kt:
+        for _ in range(args.iters):
+            codec.encode_top(g, k, packet=pkt, check=False)
+            codec.decode(pkt, out=out)
+        torch.cuda.synchronize()
+    codec.resolve([pkt])
+    res = {c: round(kt.avg_us(c), 2) for c in L.TIME_CLASSES if kt.launches.get(c)}
+    res["compact_GBps_alg"] = round((4.0 * n + 8.0 * k) / (res["compact"] * 1e-6) / 1e9, 1)
+    # FedAVG decode-accumulate of M packets (the same packet M times): per-packet cost
+    M = args.m
+    pk = [pkt] * M
+    views = codec.views_tensor(pk, [1.0 / M] * M, g.device)
+    acc = torch.empty_like(g)
+    codec.decode_accumulate(pk, [1.0 / M] * M, out=acc, views=views)
+    torch.cuda.synchronize()
+    with L.KernelTimer() as kt2:
+        for _ in range(3):
+            codec.decode_accumulate(pk, [1.0 / M] * M, out=acc, views=views)
+        torch.cuda.synchronize()
+    res["decacc_us_per_pkt"] = round(kt2.ms["decode"] * 1e3 / (3 * M), 2)
+    print(json.dumps({"tag": args.tag, "n": n, "k": k, "avg_us": res}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
