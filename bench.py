@@ -107,6 +107,7 @@ def main():
     from openmsftl_amd import _lib as L
     from openmsftl_amd import codec
     from openmsftl_amd.compression import kept_count
+    from openmsftl_amd.distributed import ShardedFedAvg, fedavg_weights, packet_fold, shard_range
 
     M, n, f = args.clients, args.n, args.fraction
     k = kept_count(f, n)
@@ -119,21 +120,25 @@ def main():
     hdrs = torch.empty((M, L.HDR_BYTES), dtype=torch.uint8, device=device)
     pkts = [codec.Packet.alloc(n, L.FC_FMT_IDXVAL, device, hdr=hdrs[i], k=k)
             for i in range(M)]
-    w = [1.0 / (M * world)] * M                 # global FedAVG weights fl32(1/#clients)
-    views = codec.views_tensor(pkts, w, device)
+    # global FedAVG weights fl32(1/#clients) (gar.py:37-40); this rank owns rows
+    # shard_range(M * world, world, rank) of G (distributed.py)
+    w_all = fedavg_weights(M * world)
+    rows = shard_range(M * world, world, rank)
+    assert len(rows) == M
+    views = codec.views_tensor(pkts, [float(x) for x in w_all[rows.start:rows.stop]], device)
+    fold = packet_fold(pkts, views)
+    fedavg = ShardedFedAvg(mode="reduce", dst=0)
     acc = torch.empty(n, dtype=torch.float32, device=device)
     redo_total = [0]
 
     def step():
         for i in range(M):
             codec.encode_top(grads[i], k, packet=pkts[i], check=False)
-        codec.decode_accumulate(pkts, w, out=acc, views=views)
         status = hdrs[:, 36:40].cpu()               # fc_packet_hdr.status (synchronises)
         if bool((status != 0).any()):               # sampled bracket missed: exact re-encode
             redo_total[0] += codec.resolve(pkts)
-            codec.decode_accumulate(pkts, w, out=acc, views=views)
-        if world > 1:
-            dist.reduce(acc, dst=0, op=dist.ReduceOp.SUM)
+        # local fold of this rank's shard (k_decode<ACC>) + RCCL fp32 reduce to rank 0
+        fedavg.aggregate(fold, M * world, acc, weights=w_all)
 
     for _ in range(args.warmup):
         step()

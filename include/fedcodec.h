@@ -147,6 +147,11 @@ int fc_decode_dense(const fc_packet_view* pkt, int format, uint64_t n, void* out
  * acc[j] = fl(w_0 * d_0[j]);  acc[j] = fl(acc[j] + fl(w_i * d_i[j])) for i = 1..m-1. */
 int fc_decode_accumulate(const fc_packet_view* views_dev, int m, int format, uint64_t n,
                          float* acc, fc_stream_t stream);
+/* Same fold, continuing the partial sum already held in acc (acc = fl(acc + fl(w_i * d_i))
+ * for i = 0..m-1): rows of G split across calls or across GPUs (the exact chained reduce of
+ * SURVEY.md §8(e)) give the same bits as one call over all rows. */
+int fc_decode_accumulate_continue(const fc_packet_view* views_dev, int m, int format,
+                                  uint64_t n, float* acc, fc_stream_t stream);
 
 /* ---- FedAVG over dense rows (gar.py:44 for 'full'): rows = DEVICE array of m row
  * pointers, w = DEVICE fp32[m]. */

@@ -230,8 +230,12 @@ def views_tensor(packets: Sequence[Packet], weights, device) -> torch.Tensor:
 
 
 def decode_accumulate(packets: Sequence[Packet], weights, out: Optional[torch.Tensor] = None,
-                      views: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """FedAVG over packets: bit-exact ``np.sum(G * w[:, None], axis=0)`` (gar.py:44)."""
+                      views: Optional[torch.Tensor] = None,
+                      continue_sum: bool = False) -> torch.Tensor:
+    """FedAVG over packets: bit-exact ``np.sum(G * w[:, None], axis=0)`` (gar.py:44).
+
+    ``continue_sum=True`` folds the packets into the partial sum already in ``out`` (rows of
+    G that an earlier call, or an earlier rank of the chained reduce, has summed)."""
     lib = L.load()
     if not packets:
         raise ValueError("no packets")
@@ -239,10 +243,16 @@ def decode_accumulate(packets: Sequence[Packet], weights, out: Optional[torch.Te
     if any(p.fmt != fmt or p.n != n for p in packets):
         raise ValueError("packets must share n and format")
     if out is None:
+        if continue_sum:
+            raise ValueError("continue_sum needs the partial sum in `out`")
         out = torch.empty(n, dtype=torch.float32, device=dev)
+    _require_cuda_f32(out, "out")
+    if out.numel() != n:
+        raise ValueError("out must have n elements")
     if views is None:
         views = views_tensor(packets, weights, dev)
-    L.check(lib.fc_decode_accumulate(_vp(views), len(packets), fmt, n, _vp(out), _stream(dev)),
+    fn = lib.fc_decode_accumulate_continue if continue_sum else lib.fc_decode_accumulate
+    L.check(fn(_vp(views), len(packets), fmt, n, _vp(out), _stream(dev)),
             "fc_decode_accumulate")
     return out
 

@@ -356,8 +356,8 @@ int fc_decode_dense(const fc_packet_view* pkt, int format, uint64_t n, void* out
   return FC_OK;
 }
 
-int fc_decode_accumulate(const fc_packet_view* views_dev, int m, int format, uint64_t n,
-                         float* acc, fc_stream_t stream) {
+static int decode_accumulate(const fc_packet_view* views_dev, int m, int format, uint64_t n,
+                             float* acc, bool cont, fc_stream_t stream) {
   FC_CHECK(views_dev && acc, "NULL argument");
   FC_CHECK(m >= 1, "m=%d < 1", m);
   FC_CHECK(n >= 1 && n <= 0xffffffffull, "bad n");
@@ -369,7 +369,7 @@ int fc_decode_accumulate(const fc_packet_view* views_dev, int m, int format, uin
   for (int m0 = 0; m0 < m; m0 += kDecMaxM) {
     DecodeArgs a;
     memset(&a, 0, sizeof a);
-    a.views = views_dev + m0; a.m = std::min(m - m0, kDecMaxM); a.acc_in = m0 > 0;
+    a.views = views_dev + m0; a.m = std::min(m - m0, kDecMaxM); a.acc_in = cont || m0 > 0;
     a.n = n; a.out = acc;
     TimedLaunch t(FC_TIME_DECODE, s);
     if (format == FC_FMT_IDXVAL) hipLaunchKernelGGL((k_decode<FC_FMT_IDXVAL, true, false>), grid, blk, 0, s, a);
@@ -377,6 +377,16 @@ int fc_decode_accumulate(const fc_packet_view* views_dev, int m, int format, uin
     FC_LAUNCHED("k_decode(acc)");
   }
   return FC_OK;
+}
+
+int fc_decode_accumulate(const fc_packet_view* views_dev, int m, int format, uint64_t n,
+                         float* acc, fc_stream_t stream) {
+  return decode_accumulate(views_dev, m, format, n, acc, false, stream);
+}
+
+int fc_decode_accumulate_continue(const fc_packet_view* views_dev, int m, int format,
+                                  uint64_t n, float* acc, fc_stream_t stream) {
+  return decode_accumulate(views_dev, m, format, n, acc, true, stream);
 }
 
 int fc_weighted_sum_dense(const float* const* rows, const float* w, int m, uint64_t n,

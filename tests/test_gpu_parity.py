@@ -287,6 +287,31 @@ def test_fedavg_packets_bit_exact(M, n, f):
     assert agg.tobytes() == ref.tobytes()
 
 
+@pytest.mark.parametrize("split", [1, 5, 70])
+def test_fedavg_continue_equals_one_call(split):
+    """fc_decode_accumulate_continue: rows split across calls (or ranks of the chained
+    reduce, distributed.py) fold to the same bits as one call; > 64 rows span launches."""
+    codec = _codec()
+    M, n, f = 96, 40_961, 0.05
+    rng = np.random.default_rng(split)
+    grads = [(rng.standard_normal(n) * 10.0 ** rng.uniform(-4, -1)).astype(np.float32)
+             for _ in range(M)]
+    k = co.num_kept(f, n)
+    pkts = [codec.encode_top(torch.from_numpy(x).cuda(), k) for x in grads]
+    w = list(np.full(M, 1.0 / M, np.float32))
+    one = codec.decode_accumulate(pkts, w).cpu().numpy()
+    acc = codec.decode_accumulate(pkts[:split], w[:split])
+    codec.decode_accumulate(pkts[split:], w[split:], out=acc, continue_sum=True)
+    assert acc.cpu().numpy().tobytes() == one.tobytes()
+    from openmsftl_amd.distributed import ShardedFedAvg, packet_fold
+    out = torch.empty(n, dtype=torch.float32, device="cuda")
+    ShardedFedAvg().aggregate(packet_fold(pkts), M, out)       # world 1: plain fold
+    assert out.cpu().numpy().tobytes() == one.tobytes()
+    Gd = go.build_dense_G([co.compress({"compression_function": "top",
+                                        "fraction_coordinate": f}, x) for x in grads], np.float32)
+    assert one.tobytes() == go.FedAvgOracle({}).aggregate(Gd).tobytes()
+
+
 def test_fedavg_packets_dropout_unbiased_and_weights():
     codec = _codec()
     L = _L()
