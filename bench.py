@@ -41,6 +41,8 @@ def parse():
     ap.add_argument("--fraction", type=float, default=0.1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-single", action="store_true", help="skip the single-gradient probe")
+    ap.add_argument("--no-batch", action="store_true",
+                    help="encode client by client (fc_topk_encode) instead of batched")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_k_compact.json"),
                     help="PMC summary (profiles/) used for roofline.traffic")
     return ap.parse_args()
@@ -82,11 +84,12 @@ def cpu_baseline(n, fraction):
 
 
 def load_pmc(path):
+    """HBM bytes per client of k_compact, from the committed rocprofv3 PMC summary."""
     try:
         with open(path) as fh:
             d = json.load(fh)
-        return d.get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
+        return d["hbm_bytes_per_launch"] / d.get("clients_per_launch", 1)
+    except (OSError, ValueError, KeyError):
         return None
 
 
@@ -127,13 +130,18 @@ def main():
     assert len(rows) == M
     views = codec.views_tensor(pkts, [float(x) for x in w_all[rows.start:rows.stop]], device)
     fold = packet_fold(pkts, views)
+    jobs = codec.encode_jobs(grads, pkts)
+    per_launch = 1 if args.no_batch else M          # clients per k_compact launch
     fedavg = ShardedFedAvg(mode="reduce", dst=0)
     acc = torch.empty(n, dtype=torch.float32, device=device)
     redo_total = [0]
 
     def step():
-        for i in range(M):
-            codec.encode_top(grads[i], k, packet=pkts[i], check=False)
+        if args.no_batch:
+            for i in range(M):
+                codec.encode_top(grads[i], k, packet=pkts[i], check=False)
+        else:                                       # 4 launches for all M clients
+            codec.encode_top_batch(grads, k, packets=pkts, jobs=jobs, check=False)
         status = hdrs[:, 36:40].cpu()               # fc_packet_hdr.status (synchronises)
         if bool((status != 0).any()):               # sampled bracket missed: exact re-encode
             redo_total[0] += codec.resolve(pkts)
@@ -166,11 +174,15 @@ def main():
 
     # roofline of the dominant kernel (k_compact: the single streaming pass over g)
     t_compact_us = kt.avg_us("compact")
-    alg_bytes = 4.0 * n + 8.0 * k                  # encode reads 4N, writes 8k
+    # the encode pass reads 4N and writes 8k per client
+    alg_bytes = per_launch * (4.0 * n + 8.0 * k)
     achieved = alg_bytes / (t_compact_us * 1e-6) / 1e9
-    roofline = {"kernel": "fc::k_compact<0,0,0> (top-k encode pass)", "bound": "hbm",
+    pmc = load_pmc(args.pmc)
+    roofline = {"kernel": "fc::k_compact<0,0,0> (top-k encode pass, %d client(s) per launch)"
+                          % per_launch, "bound": "hbm",
                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": load_pmc(args.pmc),
+                "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                "traffic": int(pmc * per_launch) if pmc else None,
                 "alg_bytes_per_launch": int(alg_bytes), "avg_launch_us": round(t_compact_us, 2),
                 "launches": kt.launches.get("compact", 0)}
     breakdown = {c: {"avg_us": round(kt.avg_us(c), 2), "launches": kt.launches[c],

@@ -120,6 +120,28 @@ int fc_topk_encode(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_
                    uint64_t offset, uint32_t* idx, float* val, uint64_t capacity,
                    uint32_t* cnt, fc_packet_hdr* hdr, void* ws, size_t ws_bytes,
                    fc_stream_t stream);
+/* ---- batched top-k / native rand-k: M clients, one launch per pipeline stage ----------
+ * The same fast path as fc_topk_encode for m gradients of equal length n, with the grid's
+ * y dimension indexing the client: 4 launches for the whole batch instead of 4 per client,
+ * so the small sampling / resolve stages of all clients overlap.  jobs: DEVICE array of m
+ * fc_encode_job; ws: fc_workspace_bytes_batch(n, m) bytes, zeroed once with
+ * fc_workspace_init.  Requires 0 < k < n (trivial k: fc_topk_encode).  A packet whose header
+ * reports FC_STATUS_RETRY_EXACT is re-encoded with fc_topk_encode_exact, as for one client. */
+typedef struct fc_encode_job {
+  const float* g;        /* gradient, 16-B aligned                          */
+  uint32_t* idx;         /* packet buffers (capacity >= fc_packet_capacity) */
+  float* val;
+  uint32_t* cnt;
+  fc_packet_hdr* hdr;
+  uint64_t seed;         /* Philox key / counter (FC_KEY_PHILOX)            */
+  uint64_t offset;
+  uint64_t reserved;
+} fc_encode_job;         /* 64 bytes */
+size_t fc_workspace_bytes_batch(uint64_t n, int m);
+int fc_topk_encode_batch(const fc_encode_job* jobs_dev, int m, uint64_t n, uint64_t k,
+                         int key_mode, uint64_t capacity, void* ws, size_t ws_bytes,
+                         fc_stream_t stream);
+
 /* Exact radix-select path (several reads of g); always succeeds; n_entries == k. */
 int fc_topk_encode_exact(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_t seed,
                          uint64_t offset, uint32_t* idx, float* val, uint64_t capacity,

@@ -49,7 +49,15 @@ class PacketView(ctypes.Structure):
                 ("reserved", ctypes.c_uint32)]
 
 
+class EncodeJob(ctypes.Structure):
+    _fields_ = [("g", ctypes.c_void_p), ("idx", ctypes.c_void_p), ("val", ctypes.c_void_p),
+                ("cnt", ctypes.c_void_p), ("hdr", ctypes.c_void_p),
+                ("seed", ctypes.c_uint64), ("offset", ctypes.c_uint64),
+                ("reserved", ctypes.c_uint64)]
+
+
 assert ctypes.sizeof(PacketHdr) == HDR_BYTES
+assert ctypes.sizeof(EncodeJob) == 64
 assert ctypes.sizeof(PacketView) == 48
 
 _u64, _i32, _sz, _vp, _dbl = (ctypes.c_uint64, ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p,
@@ -65,6 +73,8 @@ SIGNATURES = {
     "fc_workspace_init": (_i32, [_vp, _sz, _vp]),
     "fc_topk_encode": (_i32, [_vp, _u64, _u64, _i32, _u64, _u64, _vp, _vp, _u64, _vp, _vp,
                               _vp, _sz, _vp]),
+    "fc_workspace_bytes_batch": (_sz, [_u64, _i32]),
+    "fc_topk_encode_batch": (_i32, [_vp, _i32, _u64, _u64, _i32, _u64, _vp, _sz, _vp]),
     "fc_topk_encode_exact": (_i32, [_vp, _u64, _u64, _i32, _u64, _u64, _vp, _vp, _u64, _vp,
                                     _vp, _vp, _sz, _vp]),
     "fc_mask_encode": (_i32, [_vp, _u64, _i32, _vp, _dbl, _u64, _u64, _i32, _vp, _vp, _vp,

@@ -160,6 +160,88 @@ def encode_top(g: torch.Tensor, k: int, *, key_mode: int = L.FC_KEY_MAGNITUDE, s
     return packet
 
 
+class BatchWorkspace:
+    """Scratch for fc_topk_encode_batch: one encoder state per client (zeroed once)."""
+
+    _cache: dict = {}
+
+    def __init__(self, n: int, m: int, device: torch.device):
+        lib = L.load()
+        self.n, self.m = n, m
+        self.nbytes = int(lib.fc_workspace_bytes_batch(n, m))
+        self.buf = torch.empty(self.nbytes, dtype=torch.uint8, device=device)
+        L.check(lib.fc_workspace_init(_vp(self.buf), self.nbytes, _stream(device)),
+                "fc_workspace_init")
+
+    @classmethod
+    def get(cls, n: int, m: int, device: torch.device) -> "BatchWorkspace":
+        key = (device.index if device.index is not None else torch.cuda.current_device(),
+               torch.cuda.current_stream(device).cuda_stream, n)
+        ws = cls._cache.get(key)
+        if ws is None or ws.m < m:
+            ws = cls(n, m, device)
+            cls._cache[key] = ws
+        return ws
+
+
+def encode_jobs(grads: Sequence[torch.Tensor], packets: Sequence[Packet], seeds=None,
+                offsets=None) -> torch.Tensor:
+    """Device array of fc_encode_job (build once, reuse while the buffers live)."""
+    m = len(grads)
+    seeds = seeds if seeds is not None else [0] * m
+    offsets = offsets if offsets is not None else [0] * m
+    arr = (L.EncodeJob * m)(*[
+        L.EncodeJob(g=g.data_ptr(), idx=p.idx.data_ptr(), val=p.val.data_ptr(),
+                    cnt=p.cnt.data_ptr(), hdr=p.hdr.data_ptr(), seed=int(s), offset=int(o),
+                    reserved=0)
+        for g, p, s, o in zip(grads, packets, seeds, offsets)])
+    host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+    return host.to(grads[0].device)
+
+
+def encode_top_batch(grads: Sequence[torch.Tensor], k: int, *,
+                     key_mode: int = L.FC_KEY_MAGNITUDE, seeds=None, offsets=None,
+                     packets: Optional[Sequence[Packet]] = None,
+                     jobs: Optional[torch.Tensor] = None, check: bool = True) -> list:
+    """Top-k (or native rand-k) of M equal-length gradients in ONE launch per pipeline stage
+    (fc_topk_encode_batch).  Same packets, bit for bit, as M calls of :func:`encode_top`.
+    ``jobs``: a prebuilt :func:`encode_jobs` array for these exact grads/packets."""
+    if not grads:
+        raise ValueError("no gradients")
+    lib = L.load()
+    n, dev = grads[0].numel(), grads[0].device
+    for g in grads:
+        _require_cuda_f32(g)
+        if g.numel() != n or g.device != dev:
+            raise ValueError("batched gradients must share length and device")
+    if not 0 <= k <= n:
+        raise ValueError(f"k={k} outside [0, {n}]")
+    m = len(grads)
+    seeds = seeds if seeds is not None else [0] * m
+    offsets = offsets if offsets is not None else [0] * m
+    if packets is None:
+        packets = [Packet.alloc(n, L.FC_FMT_IDXVAL, dev, k=k) for _ in range(m)]
+    if len(packets) != m:
+        raise ValueError("one packet per gradient")
+    if k == 0 or k == n or n < 2:                    # trivial thresholds: exact engine per client
+        return [encode_top(g, k, key_mode=key_mode, seed=s, offset=o, packet=p, check=check)
+                for g, p, s, o in zip(grads, packets, seeds, offsets)]
+    for p, g, s, o in zip(packets, grads, seeds, offsets):
+        if p.capacity < int(lib.fc_packet_capacity(n)) or p.fmt != L.FC_FMT_IDXVAL:
+            raise ValueError("packet too small or not idx/val")
+        p.k = k
+        p._enc = (g, k, key_mode, s, o)
+    if jobs is None:
+        jobs = encode_jobs(grads, packets, seeds, offsets)
+    ws = BatchWorkspace.get(n, m, dev)
+    L.check(lib.fc_topk_encode_batch(_vp(jobs), m, n, k, key_mode, packets[0].capacity,
+                                     _vp(ws.buf), ws.nbytes, _stream(dev)),
+            "fc_topk_encode_batch")
+    if check:
+        resolve(packets)
+    return list(packets)
+
+
 def resolve(packets: Sequence[Packet]) -> int:
     """Re-encode (exact path) every top/rand packet whose sampled bracket missed.
     Returns the number of packets that needed the exact path."""

@@ -268,20 +268,90 @@ int fc_topk_encode(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_
   {
     TimedLaunch t(FC_TIME_SAMPLE, s);
     if (key_mode == FC_KEY_PHILOX) {
-      hipLaunchKernelGGL((k_sample<kKeyPhilox, 1>), dim3(sgrid), dim3(kBlock), 0, s, g, P, seed, offset, ca.W, ca.ib, hdr, hi);
+      hipLaunchKernelGGL((k_sample<kKeyPhilox, 1>), dim3(sgrid), dim3(kBlock), 0, s, g, P, seed, offset, ca.W, ca.ib, hdr, hi, nullptr, 0ull);
       FC_LAUNCHED("k_sample1");
-      hipLaunchKernelGGL((k_sample<kKeyPhilox, 2>), dim3(sgrid), dim3(kBlock), 0, s, g, P, seed, offset, ca.W, ca.ib, hdr, hi);
+      hipLaunchKernelGGL((k_sample<kKeyPhilox, 2>), dim3(sgrid), dim3(kBlock), 0, s, g, P, seed, offset, ca.W, ca.ib, hdr, hi, nullptr, 0ull);
       FC_LAUNCHED("k_sample2");
     } else {
-      hipLaunchKernelGGL((k_sample<kKeyMag, 1>), dim3(sgrid), dim3(kBlock), 0, s, g, P, seed, offset, ca.W, ca.ib, hdr, hi);
+      hipLaunchKernelGGL((k_sample<kKeyMag, 1>), dim3(sgrid), dim3(kBlock), 0, s, g, P, seed, offset, ca.W, ca.ib, hdr, hi, nullptr, 0ull);
       FC_LAUNCHED("k_sample1");
-      hipLaunchKernelGGL((k_sample<kKeyMag, 2>), dim3(sgrid), dim3(kBlock), 0, s, g, P, seed, offset, ca.W, ca.ib, hdr, hi);
+      hipLaunchKernelGGL((k_sample<kKeyMag, 2>), dim3(sgrid), dim3(kBlock), 0, s, g, P, seed, offset, ca.W, ca.ib, hdr, hi, nullptr, 0ull);
       FC_LAUNCHED("k_sample2");
     }
   }
   rc = launch_compact_key(key_mode, ca, s);
   if (rc) return rc;
   return launch_resolve(ra, s);
+}
+
+size_t fc_workspace_bytes_batch(uint64_t n, int m) {
+  return m > 0 ? (size_t)WsLayout::of(n).bytes * (size_t)m : 0;
+}
+
+int fc_topk_encode_batch(const fc_encode_job* jobs, int m, uint64_t n, uint64_t k,
+                         int key_mode, uint64_t capacity, void* ws, size_t ws_bytes,
+                         fc_stream_t stream) {
+  FC_CHECK(jobs != nullptr, "jobs is NULL");
+  FC_CHECK(m >= 1 && m <= 65535, "m=%d outside [1, 65535]", m);
+  FC_CHECK(n >= 2 && n <= 0xffffffffull, "n=%llu outside [2, 2^32-1]", (unsigned long long)n);
+  FC_CHECK(k > 0 && k < n, "batched encode needs 0 < k < n (k=%llu): use fc_topk_encode",
+           (unsigned long long)k);
+  FC_CHECK(key_mode == FC_KEY_MAGNITUDE || key_mode == FC_KEY_PHILOX, "bad key_mode %d", key_mode);
+  FC_CHECK(capacity >= fc_packet_capacity(n), "capacity %llu < fc_packet_capacity(n) %llu",
+           (unsigned long long)capacity, (unsigned long long)fc_packet_capacity(n));
+  FC_CHECK(ws != nullptr, "workspace is NULL");
+  if (ws_bytes < fc_workspace_bytes_batch(n, m))
+    return fail(FC_ERR_WORKSPACE, "workspace %zu B < %zu B needed", ws_bytes,
+                fc_workspace_bytes_batch(n, m));
+  const uint32_t ib = index_bits(n);
+  const uint64_t stride = WsLayout::of(n).bytes;
+  HdrInit hi;
+  memset(&hi, 0, sizeof hi);
+  hi.n = (uint32_t)n; hi.k = (uint32_t)k; hi.ib = ib;
+  hi.codec = key_mode == FC_KEY_PHILOX ? FC_CODEC_RAND : FC_CODEC_TOP;
+  hi.format = FC_FMT_IDXVAL; hi.key_mode = (uint32_t)key_mode;
+  CompactArgs ca;
+  memset(&ca, 0, sizeof ca);
+  ca.n = n; ca.ib = ib; ca.nchunks = num_chunks(n); ca.W = ws_ptrs(ws, n); ca.HI = hi;
+  ca.jobs = jobs; ca.ws_stride = stride;
+  ResolveArgs ra;
+  memset(&ra, 0, sizeof ra);
+  ra.ib = ib; ra.nchunks = ca.nchunks; ra.k = k; ra.key_mode = (uint32_t)key_mode;
+  ra.W = ca.W; ra.jobs = jobs; ra.ws_stride = stride;
+  hipStream_t s = (hipStream_t)stream;
+  const SamplePlan P = make_plan(n, k);
+  const dim3 sgrid((P.nseg + kSampleSegs - 1) / kSampleSegs, (uint32_t)m);
+  {
+    TimedLaunch t(FC_TIME_SAMPLE, s);
+    if (key_mode == FC_KEY_PHILOX) {
+      hipLaunchKernelGGL((k_sample<kKeyPhilox, 1>), sgrid, dim3(kBlock), 0, s, nullptr, P, 0ull, 0ull, ca.W, ib, nullptr, hi, jobs, stride);
+      FC_LAUNCHED("k_sample1(batch)");
+      hipLaunchKernelGGL((k_sample<kKeyPhilox, 2>), sgrid, dim3(kBlock), 0, s, nullptr, P, 0ull, 0ull, ca.W, ib, nullptr, hi, jobs, stride);
+      FC_LAUNCHED("k_sample2(batch)");
+    } else {
+      hipLaunchKernelGGL((k_sample<kKeyMag, 1>), sgrid, dim3(kBlock), 0, s, nullptr, P, 0ull, 0ull, ca.W, ib, nullptr, hi, jobs, stride);
+      FC_LAUNCHED("k_sample1(batch)");
+      hipLaunchKernelGGL((k_sample<kKeyMag, 2>), sgrid, dim3(kBlock), 0, s, nullptr, P, 0ull, 0ull, ca.W, ib, nullptr, hi, jobs, stride);
+      FC_LAUNCHED("k_sample2(batch)");
+    }
+  }
+  {
+    TimedLaunch t(FC_TIME_COMPACT, s);
+    const dim3 grid(ca.nchunks, (uint32_t)m);
+    if (key_mode == FC_KEY_PHILOX)
+      hipLaunchKernelGGL((k_compact<kKeyPhilox, kPredKey, FC_FMT_IDXVAL>), grid, dim3(kCBlock), 0, s, ca);
+    else
+      hipLaunchKernelGGL((k_compact<kKeyMag, kPredKey, FC_FMT_IDXVAL>), grid, dim3(kCBlock), 0, s, ca);
+    FC_LAUNCHED("k_compact(batch)");
+  }
+  {
+    TimedLaunch t(FC_TIME_ENGINE, s);
+    // fewer resolve workgroups per client than a lone encode: the batch fills the chip
+    const uint32_t rg = ca.nchunks < (uint32_t)kResolveGridBatch ? ca.nchunks : (uint32_t)kResolveGridBatch;
+    hipLaunchKernelGGL(k_resolve, dim3(rg, (uint32_t)m), dim3(kBlock), 0, s, ra);
+    FC_LAUNCHED("k_resolve(batch)");
+  }
+  return FC_OK;
 }
 
 int fc_mask_encode(const float* g, uint64_t n, int codec, const uint32_t* mask_bits, double p,

@@ -68,6 +68,20 @@ struct WsPtrs {
   uint64_t cand_cap;
 };
 
+// Batched encode: client j's workspace starts j * ws_stride bytes after client 0's.
+__device__ __forceinline__ WsPtrs ws_shift(WsPtrs W, uint64_t bytes) {
+  W.st = reinterpret_cast<TopkState*>(reinterpret_cast<char*>(W.st) + bytes);
+  W.hist1 = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(W.hist1) + bytes);
+  W.hist2h = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(W.hist2h) + bytes);
+  W.hist2l = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(W.hist2l) + bytes);
+  W.ehist = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(W.ehist) + bytes);
+  W.chist = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(W.chist) + bytes);
+  W.small = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(W.small) + bytes);
+  W.ccnt = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(W.ccnt) + bytes);
+  W.cand = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(W.cand) + bytes);
+  return W;
+}
+
 __device__ __forceinline__ void write_hdr_static(fc_packet_hdr* h, const HdrInit& hi) {
   h->thresh = 0; h->lower = 0;
   h->n = hi.n; h->k = hi.k; h->n_entries = 0; h->index_bits = hi.ib;

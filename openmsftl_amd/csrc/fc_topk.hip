@@ -94,10 +94,17 @@ template <int KM, int LEVEL>
 __global__ __launch_bounds__(kBlock) void k_sample(const float* __restrict__ g, SamplePlan P,
                                                    uint64_t seed, uint64_t off, WsPtrs W,
                                                    uint32_t ib, fc_packet_hdr* hdr,
-                                                   HdrInit HI) {
+                                                   HdrInit HI, const fc_encode_job* jobs,
+                                                   uint64_t ws_stride) {
   __shared__ uint32_t ha[kHistBins];
   __shared__ uint32_t hb[LEVEL == 2 ? kHistBins : 1];
   __shared__ uint32_t s_tmp[8], s_out[4], s_flag;
+  if (jobs) {                                   // batched: client blockIdx.y
+    const fc_encode_job& J = jobs[blockIdx.y];
+    g = J.g; hdr = J.hdr; seed = J.seed; off = J.offset;
+    HI.seed = seed; HI.offset = off;
+    W = ws_shift(W, (uint64_t)blockIdx.y * ws_stride);
+  }
   TopkState* S = W.st;
   const int tid = threadIdx.x;
   for (int b = tid; b < kHistBins; b += kBlock) { ha[b] = 0; if (LEVEL == 2) hb[b] = 0; }
@@ -218,7 +225,19 @@ struct CompactArgs {
   fc_packet_hdr* hdr;
   WsPtrs W;
   HdrInit HI;
+  const fc_encode_job* jobs;   // batched encode: client blockIdx.y overrides g / packet / W
+  uint64_t ws_stride;
 };
+
+// Per-client fields of a batched launch (jobs[blockIdx.y]); no-op for a single client.
+template <typename Args>
+__device__ __forceinline__ void apply_job(Args& a) {
+  if (!a.jobs) return;
+  const fc_encode_job& J = a.jobs[blockIdx.y];
+  a.idx = J.idx; a.val = J.val; a.cnt = J.cnt; a.hdr = J.hdr;
+  a.seed = J.seed; a.offset = J.offset;
+  a.W = ws_shift(a.W, (uint64_t)blockIdx.y * a.ws_stride);
+}
 
 // Stage the listed elements of one float4 (bits 0..3 of `bb`) at LDS positions pos, pos+1..
 // as packed {chunk-local index, value bits}.  LDS store cost is per wave instruction, not per
@@ -244,7 +263,9 @@ __device__ __forceinline__ void stage_f4(uint2* st, float4 v4, uint32_t bb, uint
 #define FC_COMPACT_WAVES_PER_EU 6
 #endif
 template <int KM, int PRED, int FMT>
-__global__ __launch_bounds__(kCBlock, FC_COMPACT_WAVES_PER_EU) void k_compact(CompactArgs a) {
+__global__ __launch_bounds__(kCBlock, FC_COMPACT_WAVES_PER_EU) void k_compact(CompactArgs a0) {
+  CompactArgs a = a0;
+  if (a.jobs) { a.g = a.jobs[blockIdx.y].g; apply_job(a); }
   __shared__ uint32_t s_ent[kCSlots], s_cnd[kCSlots], s_tot[2];
   // staging: one packed {chunk-local index, value bits} per listed element; lanes with
   // nothing left to write in a round store to their own dummy slot kStage + lane (one shared
@@ -468,11 +489,15 @@ struct ResolveArgs {
   uint32_t key_mode;
   fc_packet_hdr* hdr;
   WsPtrs W;
+  const fc_encode_job* jobs;   // batched encode (see CompactArgs)
+  uint64_t ws_stride;
 };
 
 constexpr int kResolveChunksMax = 2048;   // chunks per workgroup handled through LDS sizes
 
-__global__ __launch_bounds__(kBlock) void k_resolve(ResolveArgs a) {
+__global__ __launch_bounds__(kBlock) void k_resolve(ResolveArgs a0) {
+  ResolveArgs a = a0;
+  apply_job(a);
   __shared__ uint64_t sv[kSmallCap];                      // 32 KiB: histogram, then sort
   __shared__ uint32_t s_pre[kResolveChunksMax + 1];       // per-chunk gather sizes (prefix)
   __shared__ uint64_t s_ovf[kResolveChunksMax / 64];      // chunk overflowed its cand slot
@@ -728,10 +753,10 @@ __global__ __launch_bounds__(kBlock) void k_engine(EngineArgs a) {
 // --------------------------------------------------------------------------------------
 // explicit instantiations used by fc_capi.hip
 // --------------------------------------------------------------------------------------
-template __global__ void k_sample<kKeyMag, 1>(const float*, SamplePlan, uint64_t, uint64_t, WsPtrs, uint32_t, fc_packet_hdr*, HdrInit);
-template __global__ void k_sample<kKeyMag, 2>(const float*, SamplePlan, uint64_t, uint64_t, WsPtrs, uint32_t, fc_packet_hdr*, HdrInit);
-template __global__ void k_sample<kKeyPhilox, 1>(const float*, SamplePlan, uint64_t, uint64_t, WsPtrs, uint32_t, fc_packet_hdr*, HdrInit);
-template __global__ void k_sample<kKeyPhilox, 2>(const float*, SamplePlan, uint64_t, uint64_t, WsPtrs, uint32_t, fc_packet_hdr*, HdrInit);
+template __global__ void k_sample<kKeyMag, 1>(const float*, SamplePlan, uint64_t, uint64_t, WsPtrs, uint32_t, fc_packet_hdr*, HdrInit, const fc_encode_job*, uint64_t);
+template __global__ void k_sample<kKeyMag, 2>(const float*, SamplePlan, uint64_t, uint64_t, WsPtrs, uint32_t, fc_packet_hdr*, HdrInit, const fc_encode_job*, uint64_t);
+template __global__ void k_sample<kKeyPhilox, 1>(const float*, SamplePlan, uint64_t, uint64_t, WsPtrs, uint32_t, fc_packet_hdr*, HdrInit, const fc_encode_job*, uint64_t);
+template __global__ void k_sample<kKeyPhilox, 2>(const float*, SamplePlan, uint64_t, uint64_t, WsPtrs, uint32_t, fc_packet_hdr*, HdrInit, const fc_encode_job*, uint64_t);
 template __global__ void k_compact<kKeyMag, kPredKey, FC_FMT_IDXVAL>(CompactArgs);
 template __global__ void k_compact<kKeyPhilox, kPredKey, FC_FMT_IDXVAL>(CompactArgs);
 template __global__ void k_compact<kKeyMag, kPredMask, FC_FMT_IDXVAL>(CompactArgs);

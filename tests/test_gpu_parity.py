@@ -191,6 +191,72 @@ def test_top_128M_properties():
     assert h.n_entries - k < 0.06 * k
 
 
+# ---- batched encode (fc_topk_encode_batch) ----------------------------------------------
+def _packet_bytes(p):
+    idx, val, h = p.raw_entries()
+    return idx.tobytes(), val.tobytes(), int(h.thresh), int(h.n_entries), int(h.status)
+
+
+@pytest.mark.parametrize("n,f,M", [(100_003, 0.1, 5), (3_000_001, 0.01, 3), (1 << 20, 0.37, 4),
+                                   (8193, 0.5, 7), (2, 0.5, 2)])
+def test_batch_encode_equals_single(n, f, M):
+    codec = _codec()
+    rng = np.random.default_rng(n + M)
+    host = [(rng.standard_normal(n) * 10.0 ** rng.uniform(-4, 1)).astype(np.float32)
+            for _ in range(M)]
+    grads = [torch.from_numpy(x).cuda() for x in host]
+    k = co.effective_k(co.num_kept(f, n), n)
+    batch = codec.encode_top_batch(grads, k)
+    for x, g, pb in zip(host, grads, batch):
+        ps = codec.encode_top(g, k)
+        assert _packet_bytes(pb) == _packet_bytes(ps)
+        _check_top_packet(x, k, pb, codec.decode(pb).cpu().numpy())
+
+
+def test_batch_encode_philox_and_fallback():
+    """Native rand-k keys per client (seed/offset per job) and one client whose sampled
+    bracket misses (resolved by the per-packet exact path) inside the same batch."""
+    codec = _codec()
+    L = _L()
+    n = 4 << 20
+    k = n // 10
+    seeds, offs = [11, 12, 13], [1, 2, 3]
+    host = [np.random.default_rng(i).standard_normal(n, dtype=np.float32) for i in range(3)]
+    grads = [torch.from_numpy(x).cuda() for x in host]
+    pk = codec.encode_top_batch(grads, k, key_mode=L.FC_KEY_PHILOX, seeds=seeds, offsets=offs)
+    for x, p, s, o in zip(host, pk, seeds, offs):
+        keys = (ph.element_words(n, s, o) >> np.uint32(1)).astype(np.uint32)
+        want = po.selected_indices(keys, k)
+        assert codec.decode(p).cpu().numpy().tobytes() == po.decode_dense(n, want, x[want]).tobytes()
+    # hidden large values between sampled segments (as test_top_bracket_miss_falls_back_...)
+    nseg = max(64, min(1024, n // 32 // 1024))
+    starts = ((np.arange(nseg, dtype=np.int64) * (n - 1024)) // (nseg - 1)) & ~3
+    sampled = np.zeros(n, bool)
+    for s in starts:
+        sampled[s:s + 1024] = True
+    bad = np.zeros(n, np.float32)
+    hidden = np.nonzero(~sampled)[0]
+    bad[hidden[: n // 8]] = np.random.default_rng(0).standard_normal(n // 8).astype(np.float32)
+    host2 = [host[0], bad, host[2]]
+    grads2 = [torch.from_numpy(x).cuda() for x in host2]
+    pk2 = codec.encode_top_batch(grads2, k, check=False)
+    torch.cuda.synchronize()
+    assert codec.resolve(pk2) == 1
+    for x, p in zip(host2, pk2):
+        _check_top_packet(x, k, p, codec.decode(p).cpu().numpy())
+
+
+def test_batch_encode_arguments():
+    codec = _codec()
+    L = _L()
+    lib = L.load()
+    g = torch.zeros(1000, device="cuda")
+    with pytest.raises(ValueError):
+        codec.encode_top_batch([g, torch.zeros(999, device="cuda")], 10)
+    rc = lib.fc_topk_encode_batch(None, 1, 1000, 10, 0, 8192, None, 0, None)
+    assert rc == -1 and b"jobs" in lib.fc_last_error()
+
+
 # ---- rand ------------------------------------------------------------------------------
 @pytest.mark.parametrize("name", G.cases("rand__"))
 def test_rand_numpy_rng_golden(name):

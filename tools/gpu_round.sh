@@ -25,12 +25,12 @@ cat $OUT/bench.json
 if [ -z "$SKIP_PROF" ]; then
 echo "[gpu_round] rocprofv3 kernel stats"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof_bench -o bench -- \
-  python3 bench.py --no-cpu-baseline > $OUT/prof_bench.log 2>&1
+  python3 bench.py --no-cpu-baseline --no-single > $OUT/prof_bench.log 2>&1
 echo "[gpu_round] pmc FETCH_SIZE"
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o pmc -- \
-  python3 tools/kbench.py --iters 5 --m 4 --tag pmc > $OUT/pmc_fetch.log 2>&1
+  python3 tools/kbench.py --iters 3 --batch 4 --tag pmc > $OUT/pmc_fetch.log 2>&1
 echo "[gpu_round] pmc WRITE_SIZE"
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o pmc -- \
-  python3 tools/kbench.py --iters 5 --m 4 --tag pmc > $OUT/pmc_write.log 2>&1
+  python3 tools/kbench.py --iters 3 --batch 4 --tag pmc > $OUT/pmc_write.log 2>&1
 fi
 echo "[gpu_round] done"

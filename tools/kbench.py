@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--tag", default="")
     ap.add_argument("--m", type=int, default=64)
+    ap.add_argument("--batch", type=int, default=0)
     args = ap.parse_args()
     import torch
     from openmsftl_amd import _lib as L
@@ -29,6 +30,23 @@ def main():
     from openmsftl_amd import codec
     from openmsftl_amd.compression import kept_count
     n, k = args.n, kept_count(args.f, args.n)
+    if args.batch:                     # batched k_compact: clients per launch = --batch
+        gs = [torch.randn(n, device="cuda", generator=torch.Generator(device="cuda").manual_seed(s))
+              for s in range(args.batch)]
+        pk = codec.encode_top_batch(gs, k)
+        jobs = codec.encode_jobs(gs, pk)
+        torch.cuda.synchronize()
+        with L.KernelTimer() as kt:
+            for _ in range(args.iters):
+                codec.encode_top_batch(gs, k, packets=pk, jobs=jobs, check=False)
+            torch.cuda.synchronize()
+        codec.resolve(pk)
+        res = {c: round(kt.avg_us(c), 2) for c in L.TIME_CLASSES if kt.launches.get(c)}
+        res["compact_GBps_alg"] = round(args.batch * (4.0 * n + 8.0 * k)
+                                        / (res["compact"] * 1e-6) / 1e9, 1)
+        print(json.dumps({"tag": args.tag, "n": n, "k": k, "batch": args.batch, "avg_us": res}),
+              flush=True)
+        return
     g = torch.randn(n, device="cuda", generator=torch.Generator(device="cuda").manual_seed(1))
     pkt = codec.encode_top(g, k)
     out = torch.empty_like(g)
