@@ -147,12 +147,17 @@ static int launch_engine(int key_mode, const EngineArgs& base, int passes, hipSt
   return FC_OK;
 }
 
+// top-k compaction: k_compact_mag1, one workgroup per (chunk, client).
+static void launch_compact_mag(const CompactArgs& a, uint32_t m, hipStream_t s) {
+  hipLaunchKernelGGL(k_compact_mag1, dim3(a.nchunks, m), dim3(kCBlock), 0, s, a);
+}
+
 static int launch_compact_key(int key_mode, const CompactArgs& a, hipStream_t s) {
   TimedLaunch t(FC_TIME_COMPACT, s);
   if (key_mode == FC_KEY_PHILOX)
     hipLaunchKernelGGL((k_compact<kKeyPhilox, kPredKey, FC_FMT_IDXVAL>), dim3(a.nchunks), dim3(kCBlock), 0, s, a);
   else
-    hipLaunchKernelGGL((k_compact<kKeyMag, kPredKey, FC_FMT_IDXVAL>), dim3(a.nchunks), dim3(kCBlock), 0, s, a);
+    launch_compact_mag(a, 1, s);
   FC_LAUNCHED("k_compact");
   return FC_OK;
 }
@@ -341,7 +346,7 @@ int fc_topk_encode_batch(const fc_encode_job* jobs, int m, uint64_t n, uint64_t 
     if (key_mode == FC_KEY_PHILOX)
       hipLaunchKernelGGL((k_compact<kKeyPhilox, kPredKey, FC_FMT_IDXVAL>), grid, dim3(kCBlock), 0, s, ca);
     else
-      hipLaunchKernelGGL((k_compact<kKeyMag, kPredKey, FC_FMT_IDXVAL>), grid, dim3(kCBlock), 0, s, ca);
+      launch_compact_mag(ca, (uint32_t)m, s);
     FC_LAUNCHED("k_compact(batch)");
   }
   {

@@ -128,6 +128,20 @@ __device__ __forceinline__ float4 load4(const float* __restrict__ g, uint64_t e,
   if (e + 3 < n) r.w = g[e + 3];
   return r;
 }
+// Unconditional float4 load through the GLOBAL address space.  Pointers that come out of
+// memory (batched job tables) are generic to the compiler, and a generic load is a flat_load
+// that also counts in lgkmcnt; a per-element bounds branch between loads made hipcc wait for
+// each one (4 serial HBM latencies per chunk).  Callers check bounds once per chunk.
+typedef float fc_f4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const fc_f4v fc_gf4v;
+__device__ __forceinline__ float4 load4_full(const float* p) {
+#if FC_NT_LOADS
+  const fc_f4v v = __builtin_nontemporal_load((fc_gf4v*)p);
+#else
+  const fc_f4v v = *(fc_gf4v*)p;
+#endif
+  return make_float4(v.x, v.y, v.z, v.w);
+}
 __device__ __forceinline__ float f4get(const float4& v, int j) {
   return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w;
 }

@@ -279,6 +279,18 @@ __global__ __launch_bounds__(kCBlock, FC_COMPACT_WAVES_PER_EU) void k_compact(Co
   const uint32_t n32 = (uint32_t)a.n;
   if (a.write_hdr && chunk == 0 && tid == 0) write_hdr_static(a.hdr, a.HI);  // sole writer
 
+  // g first: all four loads in flight before anything waits (state loads queue behind them)
+  float4 x[kCVec];
+  if ((uint64_t)base + kChunk <= a.n) {           // block-uniform: whole chunk in range
+#pragma unroll
+    for (int i = 0; i < kCVec; ++i)
+      x[i] = load4_full(a.g + base + (uint32_t)(i * 2048 + w * 256 + lane * 4));
+  } else {
+#pragma unroll
+    for (int i = 0; i < kCVec; ++i)
+      x[i] = load4(a.g, (uint64_t)base + (uint32_t)(i * 2048 + w * 256 + lane * 4), a.n);
+  }
+
   uint32_t Lk = 0;   // key part of L64; 0xffffffff (above every key) selects nothing
   uint32_t Li = 0, t_lo = 0, t_hi = 0xffffffffu, cand_on = 0, sbin = 0;
   if (PRED == kPredKey) {
@@ -288,11 +300,6 @@ __global__ __launch_bounds__(kCBlock, FC_COMPACT_WAVES_PER_EU) void k_compact(Co
     Li = none ? 0xffffffffu : (uint32_t)(L64 & ((1ull << a.ib) - 1));
     t_lo = S->t_lo; t_hi = S->t_hi; cand_on = S->cand_on; sbin = S->sbin;
   }
-
-  float4 x[kCVec];
-#pragma unroll
-  for (int i = 0; i < kCVec; ++i)
-    x[i] = load4(a.g, (uint64_t)base + (uint32_t)(i * 2048 + w * 256 + lane * 4), a.n);
 
   // ---- predicates (branchless): bit (i*4 + j) -------------------------------------------
   uint32_t pbits = 0, cbits = 0;   // listed / candidate (or NaN stand-in for mask codecs)
@@ -470,6 +477,338 @@ __global__ __launch_bounds__(kCBlock, FC_COMPACT_WAVES_PER_EU) void k_compact(Co
     const uint32_t nb = tot_c < (uint32_t)kStage ? tot_c : (uint32_t)kStage;
     for (uint32_t t = tid; t < nb; t += kCBlock) atomicAdd(&a.W.chist[s_cbin[t]], 1u);
   }
+}
+
+// --------------------------------------------------------------------------------------
+// k_compact_mag: the top-k (|g| key) compaction in ballot form.  Element layout
+//     e = base + i*2048 + w*256 + j*64 + lane      (i < 4, w < 8, j < 4)
+// makes every (i, w, j) "group" 64 consecutive elements held one per lane in lane order, so
+// a group's listed elements are one 64-bit compare mask (SGPRs), its count one scalar
+// popcount, and a lane's position in the chunk slot = group offset + mbcnt(mask).  In the
+// common case ("fast" chunks: whole chunk in range, thresholds finite, no index tie-break
+// inside the chunk) the predicate of an element is ONE v_cmp of |g| (abs modifier) against a
+// float threshold: the k_compact float4 layout spent ~12 VALU per element on keys, validity,
+// tie-breaks and bit-field assembly and was VALU-issue-bound (146 us at 128 M vs a ~114 us
+// read+write roofline for the same bytes).
+//   listed    comp >= L64  <=>  |g| !< T_list   (NaN: unordered -> listed, as key 0x7f800001)
+//   candidate listed && key <= t_hi  <=>  |g| <= T_hi (NaN never, t_hi < +inf bits)
+// Anything else (partial chunk, the chunk holding L64's index tie-break, thresholds at or
+// above +inf bits) takes the exact integer predicate of k_compact, per element.
+// Candidates (rare) are appended through an LDS counter: k_resolve does not need them ordered.
+// --------------------------------------------------------------------------------------
+constexpr int kMGroups = 4 * kCWaves * 4;          // 128 groups of 64 elements
+constexpr int kMQ = 16;                            // groups per wave
+
+struct MagShared {
+  uint32_t gcnt[kMGroups / 4];                     // 4 group counts (bytes, <= 64) per (i, w)
+  uint32_t ncand[2];                               // candidates appended (by item parity)
+  uint32_t pad_[2];
+  uint2 st[kStage + 4];                            // packed {chunk-local index, value bits}
+  uint16_t cbin[kStage + 2];
+};
+
+// Block-uniform predicate parameters of one chunk.
+struct MagPred {
+  float T_list, T_hi;                              // fast: listed |g| !< T_list, cand |g| <= T_hi
+  uint32_t cand_all;                               // fast: t_hi >= NaN key, every listed one
+  uint32_t Lk, Li, t_lo, t_hi, cand_on, n32;       // exact (k_compact's integer form)
+};
+
+// FAST: one float compare per element.  Exact (!FAST): x[q] was replaced by the element's
+// exact predicate bits (mag_exact_bits: bit 1 listed, bit 0 candidate) and the value is
+// re-read from g when it is staged, so both paths hold the same 16 registers per lane.
+template <bool FAST>
+__device__ __forceinline__ bool mag_listed(const MagPred& P, float v) {
+  if (FAST) return !(__builtin_fabsf(v) < P.T_list);
+  return (__float_as_uint(v) >> 1) & 1u;
+}
+template <bool FAST>
+__device__ __forceinline__ bool mag_cand(const MagPred& P, float v) {
+  if (FAST) return !(__builtin_fabsf(v) < P.T_list) & ((__builtin_fabsf(v) <= P.T_hi) | (P.cand_all != 0));
+  return __float_as_uint(v) & 1u;
+}
+// k_compact's exact integer predicates (listed: comp >= L64; candidate: key in [t_lo, t_hi])
+// for element e0 + offset(q), written over x[q].
+__device__ __forceinline__ void mag_exact_bits(const MagPred& P, float (&x)[16], uint32_t e0) {
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const uint32_t e = e0 + (q >> 2) * 2048 + (q & 3) * 64;
+    const uint32_t key = mag_key(x[q]);
+    const bool valid = e < P.n32;
+    const bool p = valid & ((key > P.Lk) | ((key == P.Lk) & (e >= P.Li)));
+    const bool c = valid & (P.cand_on != 0) & (key >= P.t_lo) & (key <= P.t_hi);
+    x[q] = __uint_as_float(((uint32_t)p << 1) | (uint32_t)c);
+  }
+}
+
+// Output / workspace pointers of one item (client), built when the item is compacted: the
+// full CompactArgs of two items live across the loop spilled ~130 SGPRs.
+struct MagOut {
+  const float* g;
+  uint32_t* idx;
+  float* val;
+  uint32_t* cnt;
+  TopkState* S;
+  uint32_t* ccnt;
+  uint64_t* cand;
+  uint32_t* chist;
+  uint32_t ib;
+};
+
+template <bool FAST>
+__device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred& P,
+                                                 float (&x)[kMQ], MagShared& sh,
+                                                 uint32_t chunk, uint32_t sbin, uint32_t par) {
+  const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  const uint32_t base = chunk * (uint32_t)kChunk;
+  const uint32_t lbase = (uint32_t)(w * 256 + lane);
+#define FC_LOC(q) (lbase + ((q) >> 2) * 2048 + ((q) & 3) * 64)
+  // ---- phase 1: group counts (scalar popcounts of the compare masks) ---------------------
+  uint32_t pk[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    pk[i] = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      pk[i] |= (uint32_t)__popcll(__ballot(mag_listed<FAST>(P, x[i * 4 + j])))
+               << (8 * j);
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sh.gcnt[i * kCWaves + w] = pk[i];
+  }
+  __syncthreads();
+  // recompute the predicates in phase 2 (one v_cmp each) instead of keeping 16 compare masks
+  // live in SGPRs across the scan (that spilled 87 SGPRs)
+#pragma unroll
+  for (int q = 0; q < kMQ; ++q) asm volatile("" : "+v"(x[q]));
+  // the other parity's counter was last read before this item's barrier: reset it for the next
+  if (tid == 0) sh.ncand[par ^ 1u] = 0;
+  // every wave scans the 32 packed (i, w) words itself (no second barrier): lane L < 32 holds
+  // word L = (i, w), in element order
+  const uint32_t word = lane < kMGroups / 4 ? sh.gcnt[lane] : 0u;
+  const uint32_t sum4 = __builtin_amdgcn_sad_u8(word, 0u, 0u);      // sum of the 4 counts
+  const uint32_t incl = wave_incl_scan(sum4);
+  const uint32_t tot_e = (uint32_t)__builtin_amdgcn_readlane((int)incl, kMGroups / 4 - 1);
+  const uint32_t e0 = incl - sum4;
+  const uint32_t e1 = e0 + (word & 0xffu), e2 = e1 + ((word >> 8) & 0xffu);
+  const uint32_t e3 = e2 + ((word >> 16) & 0xffu);
+  const uint32_t o01 = e0 | (e1 << 16), o23 = e2 | (e3 << 16);
+  uint32_t goff[kMQ];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t a01 = (uint32_t)__builtin_amdgcn_readlane((int)o01, i * kCWaves + w);
+    const uint32_t a23 = (uint32_t)__builtin_amdgcn_readlane((int)o23, i * kCWaves + w);
+    goff[i * 4 + 0] = a01 & 0xffffu; goff[i * 4 + 1] = a01 >> 16;
+    goff[i * 4 + 2] = a23 & 0xffffu; goff[i * 4 + 3] = a23 >> 16;
+  }
+
+  // ---- phase 2: listed entries -> LDS stage (or straight to the slot when dense) -----------
+  const uint64_t slot = base;
+  if (tot_e <= (uint32_t)kStage) {                 // block-uniform
+#pragma unroll
+    for (int q = 0; q < kMQ; ++q) {
+      const bool p = mag_listed<FAST>(P, x[q]);
+      const uint32_t pos = prefix_count(__ballot(p)) + goff[q];
+      if (p) sh.st[pos] = make_uint2(FC_LOC(q), __float_as_uint(FAST ? x[q] : a.g[base + FC_LOC(q)]));
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < kMQ; ++q) {
+      const bool p = mag_listed<FAST>(P, x[q]);
+      const uint32_t pos = prefix_count(__ballot(p)) + goff[q];
+      if (p) {
+        a.idx[slot + pos] = base + FC_LOC(q);
+        a.val[slot + pos] = FAST ? x[q] : a.g[base + FC_LOC(q)];
+      }
+    }
+  }
+  // ---- candidates (rare; wave-uniform skip per group) ------------------------------------
+  if (P.cand_on) {
+    const uint64_t cslot = (uint64_t)chunk * kCandSlot;
+#pragma unroll
+    for (int q = 0; q < kMQ; ++q) {
+      const bool c = mag_cand<FAST>(P, x[q]);
+      const uint64_t mc = __ballot(c);
+      if (mc) {                                    // wave-uniform
+        uint32_t b0 = 0;
+        if (lane == 0) b0 = atomicAdd(&sh.ncand[par], (uint32_t)__popcll(mc));
+        const uint32_t cpos = (uint32_t)__builtin_amdgcn_readfirstlane((int)b0) + prefix_count(mc);
+        if (c) {
+          const uint32_t e = base + FC_LOC(q);
+          const uint32_t key = mag_key(FAST ? x[q] : a.g[e]);
+          if (cpos < (uint32_t)kCandSlot) a.cand[cslot + cpos] = comp_of(key, e, a.ib);
+          const uint32_t bin = (key - P.t_lo) >> sbin;
+          if (cpos < (uint32_t)kStage) sh.cbin[cpos] = (uint16_t)bin;
+          else atomicAdd(&a.chist[bin], 1u);
+        }
+      }
+    }
+  }
+#undef FC_LOC
+  __syncthreads();
+  const uint32_t tot_c = sh.ncand[par];
+  if (tid == 0) {
+    TopkState* S = a.S;
+    a.cnt[chunk] = tot_e;
+    a.ccnt[chunk] = tot_c;
+    atomicAdd(&S->shard_ent[chunk % kShards], tot_e);
+    if (tot_c) atomicAdd(&S->shard_cnd[chunk % kShards], tot_c);
+  }
+  if (tot_e <= (uint32_t)kStage) {                 // coalesced 16-B stores of the staged slot
+    for (uint32_t t = 4 * tid; t < tot_e; t += 4 * kCBlock) {
+      if (t + 4 <= tot_e) {
+        const uint4 p0 = *reinterpret_cast<const uint4*>(&sh.st[t]);
+        const uint4 p1 = *reinterpret_cast<const uint4*>(&sh.st[t + 2]);
+        *reinterpret_cast<uint4*>(a.idx + slot + t) =
+            make_uint4(base + p0.x, base + p0.z, base + p1.x, base + p1.z);
+        *reinterpret_cast<uint4*>(a.val + slot + t) = make_uint4(p0.y, p0.w, p1.y, p1.w);
+      } else {
+        for (uint32_t u = t; u < tot_e; ++u) {
+          a.idx[slot + u] = base + sh.st[u].x;
+          a.val[slot + u] = __uint_as_float(sh.st[u].y);
+        }
+      }
+    }
+  }
+  const uint32_t nb = tot_c < (uint32_t)kStage ? tot_c : (uint32_t)kStage;
+  for (uint32_t t = tid; t < nb; t += kCBlock) atomicAdd(&a.chist[sh.cbin[t]], 1u);
+}
+
+// Per-client records (job table, encoder state) are read with SCALAR loads: no kernel of this
+// launch writes them, but they sit behind generic pointers, so hipcc issued vector loads and
+// waited for them (vmcnt(0)) in front of the gradient loads: one extra serialized HBM/L2
+// latency per workgroup.  Reading through the scalar cache is fine (nothing here writes it).
+typedef uint32_t fc_u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t fc_u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t fc_u32x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ fc_u32x2 sload2(const void* p) {
+  fc_u32x2 v;
+  asm volatile("s_load_dwordx2 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
+  return v;
+}
+__device__ __forceinline__ fc_u32x4 sload4(const void* p) {
+  fc_u32x4 v;
+  asm volatile("s_load_dwordx4 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
+  return v;
+}
+__device__ __forceinline__ fc_u32x8 sload8(const void* p) {
+  fc_u32x8 v;
+  asm volatile("s_load_dwordx8 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
+  return v;
+}
+template <typename T>
+__device__ __forceinline__ T* as_ptr(uint32_t lo, uint32_t hi) {
+  return reinterpret_cast<T*>(((uint64_t)hi << 32) | lo);
+}
+
+__device__ __forceinline__ const float* mag_g(const CompactArgs& a0, uint32_t client) {
+  if (!a0.jobs) return a0.g;
+  const fc_u32x2 v = sload2(&a0.jobs[client].g);
+  return as_ptr<const float>(v.x, v.y);
+}
+__device__ __forceinline__ TopkState* mag_S(const CompactArgs& a0, uint32_t client) {
+  return reinterpret_cast<TopkState*>(reinterpret_cast<char*>(a0.W.st) + (uint64_t)client * a0.ws_stride);
+}
+__device__ __forceinline__ MagOut mag_out(const CompactArgs& a0, uint32_t client) {
+  MagOut o;
+  const WsPtrs W = a0.jobs ? ws_shift(a0.W, (uint64_t)client * a0.ws_stride) : a0.W;
+  o.g = a0.g; o.idx = a0.idx; o.val = a0.val; o.cnt = a0.cnt;
+  if (a0.jobs) {                                // {g, idx, val, cnt} = first 32 B of the job
+    const fc_u32x8 v = sload8(&a0.jobs[client]);
+    o.g = as_ptr<const float>(v[0], v[1]); o.idx = as_ptr<uint32_t>(v[2], v[3]);
+    o.val = as_ptr<float>(v[4], v[5]); o.cnt = as_ptr<uint32_t>(v[6], v[7]);
+  }
+  o.S = W.st; o.ccnt = W.ccnt; o.cand = W.cand; o.chist = W.chist; o.ib = a0.ib;
+  return o;
+}
+
+struct MagState {                                  // the encoder state k_compact_mag reads
+  uint64_t L64;
+  uint32_t t_lo, t_hi, cand_on, sbin;
+};
+static_assert(offsetof(TopkState, L64) == 8 && offsetof(TopkState, t_hi) == offsetof(TopkState, t_lo) + 4 &&
+              offsetof(TopkState, sbin) == offsetof(TopkState, t_lo) + 8 &&
+              offsetof(TopkState, cand_on) == offsetof(TopkState, t_lo) + 12 &&
+              offsetof(TopkState, t_lo) % 4 == 0, "MagState scalar-load layout");
+__device__ __forceinline__ MagState mag_state(const TopkState* S) {
+  MagState m;
+  const fc_u32x2 l = sload2(&S->L64);
+  const fc_u32x4 t = sload4(&S->t_lo);
+  m.L64 = ((uint64_t)l.y << 32) | l.x;
+  m.t_lo = t.x; m.t_hi = t.y; m.sbin = t.z; m.cand_on = t.w;
+  return m;
+}
+
+// The chunk's 16 elements per lane in the ballot layout: whole chunk = nt loads; the last,
+// partial chunk clamps its addresses (its values past n are never listed: exact path).
+__device__ __forceinline__ void mag_load(const float* g, uint32_t chunk, uint64_t n,
+                                         float (&x)[kMQ]) {
+  const uint32_t base = chunk * (uint32_t)kChunk;
+  typedef __attribute__((address_space(1))) const float gf;
+  const uint32_t l0 = (uint32_t)((threadIdx.x >> 6) * 256 + lane_id());
+  if ((uint64_t)base + kChunk > n) {
+    const uint32_t last = (uint32_t)(n - 1) - base;
+#pragma unroll
+    for (int q = 0; q < kMQ; ++q)
+      x[q] = ((gf*)g)[base + min(l0 + (q >> 2) * 2048 + (q & 3) * 64, last)];
+    return;
+  }
+  gf* gp = (gf*)g + base + l0;
+#pragma unroll
+  for (int q = 0; q < kMQ; ++q) x[q] = __builtin_nontemporal_load(gp + (q >> 2) * 2048 + (q & 3) * 64);
+}
+
+// One workgroup per item (grid = (nchunks, clients)); <= 64 VGPRs, so 4 resident 512-thread
+// workgroups per CU overlap one another's load latency.  (A persistent variant that kept the
+// next item's loads in flight measured 1.3-2.5x SLOWER: hipcc spilled the second register set
+// and loop-carried state)
+__device__ __forceinline__ void compact_mag_item(const CompactArgs& a0, uint32_t client,
+                                                 uint32_t chunk, const MagState& st,
+                                                 float (&x)[kMQ], MagShared& sh, uint32_t par) {
+  const int tid = threadIdx.x;
+  const uint32_t base = chunk * (uint32_t)kChunk;
+  const bool full = (uint64_t)base + kChunk <= a0.n;
+  const bool none = st.L64 == kSelectNothing;
+  MagPred P;
+  P.t_lo = st.t_lo; P.t_hi = st.t_hi; P.cand_on = st.cand_on; P.n32 = (uint32_t)a0.n;
+  P.Lk = none ? 0xffffffffu : (uint32_t)(st.L64 >> a0.ib);
+  P.Li = none ? 0xffffffffu : (uint32_t)(st.L64 & ((1ull << a0.ib) - 1));
+  // every element of the chunk is listed iff key >= Lk_eff when the tie-break index Li lies
+  // outside the chunk
+  const uint32_t Lk_eff = base >= P.Li ? P.Lk : P.Lk + 1u;
+  const bool tie_inside = !none && base < P.Li && (uint64_t)base + kChunk > P.Li;
+  const bool fast = full && !none && !tie_inside && Lk_eff <= 0x7f800000u;
+  P.T_list = __uint_as_float(fast ? Lk_eff : 0u);
+  // candidates: listed && key <= t_hi (t_hi >= the NaN key: every listed element)
+  P.cand_all = P.t_hi >= 0x7f800001u;
+  P.T_hi = __uint_as_float(P.cand_all ? 0x7f800000u : P.t_hi);
+  const MagOut o = mag_out(a0, client);
+  if (fast) {
+    compact_mag_body<true>(o, P, x, sh, chunk, st.sbin, par);
+  } else if (none) {                                       // k = 0: nothing listed
+    __syncthreads();
+    if (tid == 0) {
+      o.cnt[chunk] = 0;
+      o.ccnt[chunk] = 0;
+    }
+  } else {                                                 // rare: exact integer predicate
+    mag_exact_bits(P, x, base + (uint32_t)((tid >> 6) * 256 + lane_id()));
+    compact_mag_body<false>(o, P, x, sh, chunk, st.sbin, par);
+  }
+}
+
+#ifndef FC_MAG1_WAVES_PER_EU
+#define FC_MAG1_WAVES_PER_EU 8
+#endif
+__global__ __launch_bounds__(kCBlock, FC_MAG1_WAVES_PER_EU) void k_compact_mag1(CompactArgs a0) {
+  __shared__ __attribute__((aligned(16))) MagShared sh;
+  const uint32_t client = blockIdx.y, chunk = blockIdx.x;
+  float x[kMQ];
+  mag_load(mag_g(a0, client), chunk, a0.n, x);             // g first, state behind it
+  const MagState st = mag_state(mag_S(a0, client));
+  if (threadIdx.x == 0) sh.ncand[0] = 0;
+  compact_mag_item(a0, client, chunk, st, x, sh, 0u);
 }
 
 // --------------------------------------------------------------------------------------
