@@ -62,12 +62,12 @@ static WsPtrs ws_ptrs(void* ws, uint64_t n) {
 // 64..1024 segments of 1024 (n/32 .. 1 M keys) and a +-6 sigma binomial margin.
 // Persistent decode grid: every workgroup resident (4 per CU at ~38 KiB LDS), each walking
 // ceil(chunks / grid) chunks.  FC_DECODE_GRID overrides (tuning only).
-static uint32_t decode_grid(uint64_t n) {
+static uint32_t decode_grid(uint64_t n, uint32_t per_cu = kDecBlocksPerCU) {
   static const uint32_t forced = [] {
     const char* e = getenv("FC_DECODE_GRID");
     return e ? (uint32_t)atoi(e) : 0u;
   }();
-  uint32_t g = forced ? forced : 256u * kDecBlocksPerCU;
+  uint32_t g = forced ? forced : 256u * per_cu;
   const uint32_t nch = num_chunks(n);
   return g < nch ? g : nch;
 }
@@ -422,7 +422,7 @@ int fc_decode_dense(const fc_packet_view* pkt, int format, uint64_t n, void* out
   TimedLaunch t(FC_TIME_DECODE, s);
   if (format == FC_FMT_IDXVAL) {
     if (out_f64) hipLaunchKernelGGL((k_decode<FC_FMT_IDXVAL, false, true>), grid, blk, 0, s, a);
-    else hipLaunchKernelGGL((k_decode<FC_FMT_IDXVAL, false, false>), grid, blk, 0, s, a);
+    else hipLaunchKernelGGL(k_decode_sparse<false>, dim3(decode_grid(n, kSBlocksPerCU)), dim3(kSBlock), 0, s, a);
   } else {
     if (out_f64) hipLaunchKernelGGL((k_decode<FC_FMT_BITMAP, false, true>), grid, blk, 0, s, a);
     else hipLaunchKernelGGL((k_decode<FC_FMT_BITMAP, false, false>), grid, blk, 0, s, a);
@@ -447,7 +447,8 @@ static int decode_accumulate(const fc_packet_view* views_dev, int m, int format,
     a.views = views_dev + m0; a.m = std::min(m - m0, kDecMaxM); a.acc_in = cont || m0 > 0;
     a.n = n; a.out = acc;
     TimedLaunch t(FC_TIME_DECODE, s);
-    if (format == FC_FMT_IDXVAL) hipLaunchKernelGGL((k_decode<FC_FMT_IDXVAL, true, false>), grid, blk, 0, s, a);
+    if (format == FC_FMT_IDXVAL)
+      hipLaunchKernelGGL(k_decode_sparse<true>, dim3(decode_grid(n, kSBlocksPerCU)), dim3(kSBlock), 0, s, a);
     else hipLaunchKernelGGL((k_decode<FC_FMT_BITMAP, true, false>), grid, blk, 0, s, a);
     FC_LAUNCHED("k_decode(acc)");
   }

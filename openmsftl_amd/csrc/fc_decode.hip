@@ -164,6 +164,9 @@ __device__ __forceinline__ PktCache meta_pkt(const DecMeta& pm) {
   return c;
 }
 
+struct SparseMeta;
+__device__ __forceinline__ PktCache meta_pkt_s(const SparseMeta& m);
+
 // Persistent, software-pipelined decode.  Workgroup b owns chunks b, b + G, ...; for every
 // chunk it walks the packets in G's row order (gar.py:44), one "item" (packet, chunk) at a
 // time.  Items are taken kDecGroup at a time: the group's loads (entry count, first 1024
@@ -352,6 +355,222 @@ __global__ __launch_bounds__(kDBlock, kDecBlocksPerCU) void k_decode(DecodeArgs 
   }
 }
 
+// --------------------------------------------------------------------------------------
+// k_decode_sparse<ACC>: FC_FMT_IDXVAL packets, fp32 result.  The chunk's result lives in an
+// LDS tile; each packet's kept entries are folded into it in G's row order:
+//     tile[loc] = fl(tile[loc] + fl(w * v))            (ACC; __fmul_rn / __fadd_rn)
+//     tile[loc] = v                                     (!ACC, single packet: the dense decode)
+// so the work per packet is proportional to its entries (k), not to N: k_decode<ACC> folded
+// all 8192 elements of the chunk per packet and was VALU/LDS-bound at ~38 us per 128 M packet.
+//
+// Skipping the dropped coordinates' +0 terms is exact except for the sign of zero: x + (+0)
+// == x for every x but -0.  A running sum can only BE -0 while every term so far was -0
+// (nonzero terms never cancel to -0 under RN, and +0 + -0 == +0), so the tile starts at -0 (the
+// additive identity: -0 + t == t for every t) and, for elements whose sum is -0 after a fold,
+// counts the folds (cnt8, rare path).  At write-out a -0 that was not folded by every packet
+// becomes +0 — exactly the dense sum of gar.py:44 over G.
+// A dropout-unbiased packet with p == 0 drops everything to 0/0 = NaN (compression.py:60):
+// the sum is NaN everywhere.
+//
+// Loads: every item (packet, chunk) reads its first 1024 slot entries with addresses clamped
+// to the slot's count (lanes past it re-read entry 0: no extra HBM traffic, no divergent
+// branch, exact vmcnt waits); the counts are loaded one group of items ahead.
+// --------------------------------------------------------------------------------------
+constexpr int kSBlock = 256;
+constexpr int kSR = 4;                         // entries per thread per item (1024 per item)
+constexpr int kSGroup = 4;                     // items whose loads are issued together
+constexpr int kSBlocksPerCU = 3;               // 41 KB LDS per workgroup
+
+struct SparseMeta {
+  const uint32_t* idx;
+  const float* val;
+  const uint32_t* cnt;
+  uint64_t seed, offset;
+  double p;
+  uint64_t thresh;
+  float w;
+  uint32_t flags;             // ib | codec << 8 | key_mode << 16
+};
+
+__device__ __forceinline__ PktCache meta_pkt_s(const SparseMeta& pm) {
+  PktCache c;
+  c.idx = pm.idx; c.val = pm.val; c.bitmap = pm.idx; c.cnt = pm.cnt; c.w = pm.w;
+  c.thresh = pm.thresh;
+  c.ib = pm.flags & 0xffu; c.codec = (pm.flags >> 8) & 0xffu; c.key_mode = pm.flags >> 16;
+  c.seed = pm.seed; c.offset = pm.offset; c.p = pm.p;
+  return c;
+}
+
+template <bool ACC>
+__global__ __launch_bounds__(kSBlock, kSBlocksPerCU) void k_decode_sparse(DecodeArgs a) {
+  __shared__ __attribute__((aligned(16))) float tile[kChunk];
+  __shared__ __attribute__((aligned(16))) uint8_t cnt8[ACC ? kChunk : 16];
+  __shared__ SparseMeta s_meta[ACC ? kDecMaxM : 1];
+  __shared__ uint32_t s_poison;
+  const int tid = threadIdx.x;
+  const uint32_t M = ACC ? (uint32_t)a.m : 1u;
+  const uint32_t nch = (uint32_t)((a.n + kChunk - 1) / kChunk);
+  const uint32_t G = gridDim.x;
+  if (blockIdx.x >= nch) return;
+  const uint32_t J = (nch - blockIdx.x + G - 1) / G;             // chunks of this workgroup
+  const uint32_t T = J * M;                                      // items (chunk-major)
+
+  if (tid == 0) s_poison = 0;
+  __syncthreads();
+  if (tid < (int)M) {
+    const fc_packet_view v = ACC ? a.views[tid] : a.one;
+    const fc_packet_hdr* h = v.hdr;
+    SparseMeta d;
+    d.idx = v.idx; d.val = v.val; d.cnt = v.cnt;
+    d.seed = h->seed; d.offset = h->offset; d.p = h->p;
+    d.thresh = h->thresh; d.w = v.weight;
+    d.flags = (h->index_bits & 0xffu) | ((h->codec & 0xffu) << 8) | (h->key_mode << 16);
+    s_meta[tid] = d;
+    if (h->codec == FC_CODEC_DROPOUT_UNBIASED && h->p == 0.0) atomicOr(&s_poison, 1u);
+  }
+  __syncthreads();
+  const bool poison = s_poison != 0;
+
+  // ---- per-chunk tile init / write-out (each thread owns elements tid*4 + i*1024) ----------
+  auto init_tile = [&](uint32_t c) {
+    const uint64_t base = (uint64_t)c * kChunk;
+    float dz = -0.0f;                                            // identity of the fold
+    if (!ACC) dz = dropped_f32(meta_pkt_s(s_meta[0]));
+#pragma unroll
+    for (int i = 0; i < kChunk / (kSBlock * 4); ++i) {
+      const uint32_t loc = (uint32_t)(i * 1024 + tid * 4);
+      float4 v = make_float4(dz, dz, dz, dz);
+      if (ACC && a.acc_in) v = load4(reinterpret_cast<const float*>(a.out), base + loc, a.n);
+      *reinterpret_cast<float4*>(&tile[loc]) = v;
+      if (ACC) *reinterpret_cast<uint32_t*>(&cnt8[loc]) = 0u;
+    }
+  };
+  auto write_tile = [&](uint32_t c) {
+    const uint64_t base = (uint64_t)c * kChunk;
+    float* out = reinterpret_cast<float*>(a.out);
+#pragma unroll
+    for (int i = 0; i < kChunk / (kSBlock * 4); ++i) {
+      const uint32_t loc = (uint32_t)(i * 1024 + tid * 4);
+      float4 v = *reinterpret_cast<const float4*>(&tile[loc]);
+      if (ACC) {
+        const uint32_t c4 = *reinterpret_cast<const uint32_t*>(&cnt8[loc]);
+        // -0 that some packet of this launch did not fold: the dense sum added +0 there
+        auto fix = [&](float x, uint32_t cn) {
+          return (__float_as_uint(x) == 0x80000000u && cn < M) ? 0.0f : x;
+        };
+        v = make_float4(fix(v.x, c4 & 0xffu), fix(v.y, (c4 >> 8) & 0xffu),
+                        fix(v.z, (c4 >> 16) & 0xffu), fix(v.w, c4 >> 24));
+        if (poison) v = make_float4(__uint_as_float(0x7fc00000u), __uint_as_float(0x7fc00000u),
+                                    __uint_as_float(0x7fc00000u), __uint_as_float(0x7fc00000u));
+      }
+      store_out(out, base + loc, a.n, v);
+    }
+  };
+
+  // ---- item loads: counts one group ahead, entries clamped to the count -------------------
+  auto item_chunk = [&](uint32_t t) { return blockIdx.x + (t / M) * G; };
+  auto load_cnt = [&](uint32_t t) -> uint32_t {                  // uniform value, vector load
+    const uint32_t tt = t < T ? t : T - 1;
+    const SparseMeta& pm = s_meta[tt % M];
+    return ((gu32*)uni_ptr(pm.cnt))[item_chunk(tt)];
+  };
+  uint32_t cntg[kSGroup];
+#pragma unroll
+  for (int d = 0; d < kSGroup; ++d) cntg[d] = load_cnt((uint32_t)d);
+
+  init_tile(blockIdx.x);
+  __syncthreads();
+  for (uint32_t t0 = 0; t0 < T; t0 += kSGroup) {
+    uint32_t ids[kSGroup][kSR];
+    float vs[kSGroup][kSR];
+    uint32_t cn[kSGroup];
+#pragma unroll
+    for (int d = 0; d < kSGroup; ++d) {
+      const uint32_t t = min(t0 + d, T - 1);                     // past the end: ignored
+      const SparseMeta& pm = s_meta[t % M];
+      const uint64_t lo = (uint64_t)item_chunk(t) * kChunk;
+      gf32* val = (gf32*)uni_ptr(pm.val) + lo;
+      gu32* idx = (gu32*)uni_ptr(pm.idx) + lo;
+      cn[d] = uni32(cntg[d]);
+      const uint32_t last = cn[d] ? cn[d] - 1 : 0u;
+#pragma unroll
+      for (int r = 0; r < kSR; ++r) {
+        const uint32_t e = min((uint32_t)(tid + r * kSBlock), last);
+        vs[d][r] = val[e];
+        ids[d][r] = idx[e];
+      }
+    }
+#pragma unroll
+    for (int d = 0; d < kSGroup; ++d) cntg[d] = load_cnt(t0 + kSGroup + d);   // next group
+#pragma unroll
+    for (int d = 0; d < kSGroup; ++d) {
+      const uint32_t t = t0 + d;
+      if (t >= T) break;                                         // uniform
+      const uint32_t m = t % M;
+      const uint32_t c = item_chunk(t);
+      const uint64_t base = (uint64_t)c * kChunk;
+      const SparseMeta pm = s_meta[m];
+      const float w = __uint_as_float(uni32(__float_as_uint(pm.w)));
+      const uint64_t thresh = uni64(pm.thresh);
+      const uint32_t flags = uni32(pm.flags);
+      const uint32_t ib = flags & 0xffu, codec = (flags >> 8) & 0xffu, key_mode = flags >> 16;
+      const bool scale = codec == FC_CODEC_DROPOUT_UNBIASED;     // fl32(fl64(g)/p), :60
+      const bool generic = scale || (key_mode == FC_KEY_PHILOX && thresh != 0);
+      auto fold = [&](uint32_t id, float v) {
+        const uint32_t loc = id - (uint32_t)base;
+        if (loc >= (uint32_t)kChunk) return;
+        if (ACC) {
+          const float term = __fmul_rn(v, w);
+          const float s2 = __fadd_rn(tile[loc], term);
+          tile[loc] = s2;
+          if (__float_as_uint(s2) == 0x80000000u) cnt8[loc] = (uint8_t)(cnt8[loc] + 1u);
+        } else {
+          tile[loc] = v;
+        }
+      };
+      if (!generic) {                                            // top-k / dropout-biased
+#pragma unroll
+        for (int r = 0; r < kSR; ++r) {
+          const uint32_t e = (uint32_t)(tid + r * kSBlock);
+          const uint32_t id = ids[d][r];
+          const float v = vs[d][r];
+          const bool keep = thresh == 0 || comp_of(mag_key(v), id, ib) >= thresh;
+          if (e < cn[d] && keep) fold(id, v);
+        }
+      } else {
+        const PktCache pk = meta_pkt_s(pm);
+        for (int r = 0; r < kSR; ++r) {
+          const uint32_t e = (uint32_t)(tid + r * kSBlock);
+          const uint32_t id = ids[d][r];
+          const float v = vs[d][r];
+          if (e < cn[d] && entry_kept(pk, id, v)) fold(id, scale ? (float)((double)v / pk.p) : v);
+        }
+      }
+      if (cn[d] > (uint32_t)(kSR * kSBlock)) {                   // dense slot (uniform, rare)
+        const PktCache pk = meta_pkt_s(pm);
+        gf32* pval = (gf32*)uni_ptr(pm.val) + base;
+        gu32* pidx = (gu32*)uni_ptr(pm.idx) + base;
+        for (uint32_t e = (uint32_t)(kSR * kSBlock + tid); e < cn[d]; e += kSBlock) {
+          const uint32_t id = pidx[e];
+          const float v = pval[e];
+          if (entry_kept(pk, id, v)) fold(id, scale ? (float)((double)v / pk.p) : v);
+        }
+        __builtin_amdgcn_s_waitcnt(0x0F70);                      // vmcnt(0): none left pending
+      }
+      __syncthreads();                                           // packet m folded
+      if (m + 1 == M) {                                          // chunk done
+        write_tile(c);
+        const uint32_t cnext = c + G;
+        if (t + 1 < T) {
+          __syncthreads();                                       // write-out read the tile
+          init_tile(cnext);
+          __syncthreads();
+        }
+      }
+    }
+  }
+}
+
 // Dense FedAVG over M row pointers (gar.py:44 with 'full' rows): one float4 per thread.
 __global__ __launch_bounds__(kBlock) void k_wsum(const float* const* rows, const float* w,
                                                  int m, uint64_t n, float* out) {
@@ -387,6 +606,8 @@ template __global__ void k_decode<FC_FMT_IDXVAL, false, true>(DecodeArgs);
 template __global__ void k_decode<FC_FMT_BITMAP, false, false>(DecodeArgs);
 template __global__ void k_decode<FC_FMT_BITMAP, false, true>(DecodeArgs);
 template __global__ void k_decode<FC_FMT_IDXVAL, true, false>(DecodeArgs);
+template __global__ void k_decode_sparse<true>(DecodeArgs);
+template __global__ void k_decode_sparse<false>(DecodeArgs);
 template __global__ void k_decode<FC_FMT_BITMAP, true, false>(DecodeArgs);
 
 }  // namespace fc
