@@ -363,14 +363,17 @@ __global__ __launch_bounds__(kDBlock, kDecBlocksPerCU) void k_decode(DecodeArgs 
 // so the work per packet is proportional to its entries (k), not to N: k_decode<ACC> folded
 // all 8192 elements of the chunk per packet and was VALU/LDS-bound at ~38 us per 128 M packet.
 //
-// Skipping the dropped coordinates' +0 terms is exact except for the sign of zero: x + (+0)
-// == x for every x but -0.  A running sum can only BE -0 while every term so far was -0
-// (nonzero terms never cancel to -0 under RN, and +0 + -0 == +0), so the tile starts at -0 (the
-// additive identity: -0 + t == t for every t) and, for elements whose sum is -0 after a fold,
-// counts the folds (cnt8, rare path).  At write-out a -0 that was not folded by every packet
-// becomes +0 — exactly the dense sum of gar.py:44 over G.
-// A dropout-unbiased packet with p == 0 drops everything to 0/0 = NaN (compression.py:60):
-// the sum is NaN everywhere.
+// A dropped coordinate of packet i adds the term d_i = fl(dz * w_i) (dz = +0, the dropped
+// value; NaN for dropout-unbiased with p == 0).  Skipping it is exact unless:
+//   class A, d_i == +0 (w_i >= +0): x + (+0) == x for every x but -0.  A running sum can only
+//     BE -0 while every term so far was -0 (nonzero terms never cancel to -0 under RN, and
+//     +0 + -0 == +0), so the tile starts at -0 (the additive identity: -0 + t == t) and, while
+//     an element's sum is -0, counts its class-A folds (cnt8, rare path).  At write-out a -0
+//     that some class-A packet did not fold becomes +0.
+//   class B, d_i == -0 (w_i <= -0): neutral for every x.
+//   class C, d_i == NaN (w_i = +-inf / NaN, or p == 0): every element the packet did not fold
+//     is NaN; counted by cntC.
+// The result is exactly the dense sum of gar.py:44 over G.
 //
 // Loads: every item (packet, chunk) reads its first 1024 slot entries with addresses clamped
 // to the slot's count (lanes past it re-read entry 0: no extra HBM traffic, no divergent
@@ -379,7 +382,7 @@ __global__ __launch_bounds__(kDBlock, kDecBlocksPerCU) void k_decode(DecodeArgs 
 constexpr int kSBlock = 256;
 constexpr int kSR = 4;                         // entries per thread per item (1024 per item)
 constexpr int kSGroup = 4;                     // items whose loads are issued together
-constexpr int kSBlocksPerCU = 3;               // 41 KB LDS per workgroup
+constexpr int kSBlocksPerCU = 3;               // 49 KB LDS per workgroup
 
 struct SparseMeta {
   const uint32_t* idx;
@@ -396,7 +399,7 @@ __device__ __forceinline__ PktCache meta_pkt_s(const SparseMeta& pm) {
   PktCache c;
   c.idx = pm.idx; c.val = pm.val; c.bitmap = pm.idx; c.cnt = pm.cnt; c.w = pm.w;
   c.thresh = pm.thresh;
-  c.ib = pm.flags & 0xffu; c.codec = (pm.flags >> 8) & 0xffu; c.key_mode = pm.flags >> 16;
+  c.ib = pm.flags & 0xffu; c.codec = (pm.flags >> 8) & 0xffu; c.key_mode = (pm.flags >> 16) & 0xffu;
   c.seed = pm.seed; c.offset = pm.offset; c.p = pm.p;
   return c;
 }
@@ -404,9 +407,10 @@ __device__ __forceinline__ PktCache meta_pkt_s(const SparseMeta& pm) {
 template <bool ACC>
 __global__ __launch_bounds__(kSBlock, kSBlocksPerCU) void k_decode_sparse(DecodeArgs a) {
   __shared__ __attribute__((aligned(16))) float tile[kChunk];
-  __shared__ __attribute__((aligned(16))) uint8_t cnt8[ACC ? kChunk : 16];
+  __shared__ __attribute__((aligned(16))) uint8_t cnt8[ACC ? kChunk : 16];   // class-A folds at -0
+  __shared__ __attribute__((aligned(16))) uint8_t cntC[ACC ? kChunk : 16];   // class-C folds
   __shared__ SparseMeta s_meta[ACC ? kDecMaxM : 1];
-  __shared__ uint32_t s_poison;
+  __shared__ uint32_t s_nA, s_nC;
   const int tid = threadIdx.x;
   const uint32_t M = ACC ? (uint32_t)a.m : 1u;
   const uint32_t nch = (uint32_t)((a.n + kChunk - 1) / kChunk);
@@ -415,7 +419,7 @@ __global__ __launch_bounds__(kSBlock, kSBlocksPerCU) void k_decode_sparse(Decode
   const uint32_t J = (nch - blockIdx.x + G - 1) / G;             // chunks of this workgroup
   const uint32_t T = J * M;                                      // items (chunk-major)
 
-  if (tid == 0) s_poison = 0;
+  if (tid == 0) { s_nA = 0; s_nC = 0; }
   __syncthreads();
   if (tid < (int)M) {
     const fc_packet_view v = ACC ? a.views[tid] : a.one;
@@ -425,11 +429,17 @@ __global__ __launch_bounds__(kSBlock, kSBlocksPerCU) void k_decode_sparse(Decode
     d.seed = h->seed; d.offset = h->offset; d.p = h->p;
     d.thresh = h->thresh; d.w = v.weight;
     d.flags = (h->index_bits & 0xffu) | ((h->codec & 0xffu) << 8) | (h->key_mode << 16);
+    // class of the packet's dropped term fl(dz * w): A +0, B -0, C NaN (bits 24-25)
+    const float dz = (h->codec == FC_CODEC_DROPOUT_UNBIASED && h->p == 0.0) ? __uint_as_float(0x7fc00000u) : 0.0f;
+    const uint32_t td = __float_as_uint(__fmul_rn(dz, v.weight));
+    const uint32_t cls = td == 0u ? 0u : td == 0x80000000u ? 1u : 2u;
+    d.flags |= cls << 24;
     s_meta[tid] = d;
-    if (h->codec == FC_CODEC_DROPOUT_UNBIASED && h->p == 0.0) atomicOr(&s_poison, 1u);
+    if (cls == 0u) atomicAdd(&s_nA, 1u);
+    if (cls == 2u) atomicAdd(&s_nC, 1u);
   }
   __syncthreads();
-  const bool poison = s_poison != 0;
+  const uint32_t nA = s_nA, nC = s_nC;
 
   // ---- per-chunk tile init / write-out (each thread owns elements tid*4 + i*1024) ----------
   auto init_tile = [&](uint32_t c) {
@@ -442,7 +452,10 @@ __global__ __launch_bounds__(kSBlock, kSBlocksPerCU) void k_decode_sparse(Decode
       float4 v = make_float4(dz, dz, dz, dz);
       if (ACC && a.acc_in) v = load4(reinterpret_cast<const float*>(a.out), base + loc, a.n);
       *reinterpret_cast<float4*>(&tile[loc]) = v;
-      if (ACC) *reinterpret_cast<uint32_t*>(&cnt8[loc]) = 0u;
+      if (ACC) {
+        *reinterpret_cast<uint32_t*>(&cnt8[loc]) = 0u;
+        if (nC) *reinterpret_cast<uint32_t*>(&cntC[loc]) = 0u;
+      }
     }
   };
   auto write_tile = [&](uint32_t c) {
@@ -454,14 +467,15 @@ __global__ __launch_bounds__(kSBlock, kSBlocksPerCU) void k_decode_sparse(Decode
       float4 v = *reinterpret_cast<const float4*>(&tile[loc]);
       if (ACC) {
         const uint32_t c4 = *reinterpret_cast<const uint32_t*>(&cnt8[loc]);
-        // -0 that some packet of this launch did not fold: the dense sum added +0 there
-        auto fix = [&](float x, uint32_t cn) {
-          return (__float_as_uint(x) == 0x80000000u && cn < M) ? 0.0f : x;
+        const uint32_t k4 = nC ? *reinterpret_cast<const uint32_t*>(&cntC[loc]) : 0u;
+        // -0 that some class-A packet did not fold: the dense sum added +0 there; an element
+        // some class-C packet did not fold: the dense sum added NaN there
+        auto fix = [&](float x, uint32_t cn, uint32_t kc) {
+          if (kc < nC) return __uint_as_float(0x7fc00000u);
+          return (__float_as_uint(x) == 0x80000000u && cn < nA) ? 0.0f : x;
         };
-        v = make_float4(fix(v.x, c4 & 0xffu), fix(v.y, (c4 >> 8) & 0xffu),
-                        fix(v.z, (c4 >> 16) & 0xffu), fix(v.w, c4 >> 24));
-        if (poison) v = make_float4(__uint_as_float(0x7fc00000u), __uint_as_float(0x7fc00000u),
-                                    __uint_as_float(0x7fc00000u), __uint_as_float(0x7fc00000u));
+        v = make_float4(fix(v.x, c4 & 0xffu, k4 & 0xffu), fix(v.y, (c4 >> 8) & 0xffu, (k4 >> 8) & 0xffu),
+                        fix(v.z, (c4 >> 16) & 0xffu, (k4 >> 16) & 0xffu), fix(v.w, c4 >> 24, k4 >> 24));
       }
       store_out(out, base + loc, a.n, v);
     }
@@ -513,7 +527,8 @@ __global__ __launch_bounds__(kSBlock, kSBlocksPerCU) void k_decode_sparse(Decode
       const float w = __uint_as_float(uni32(__float_as_uint(pm.w)));
       const uint64_t thresh = uni64(pm.thresh);
       const uint32_t flags = uni32(pm.flags);
-      const uint32_t ib = flags & 0xffu, codec = (flags >> 8) & 0xffu, key_mode = flags >> 16;
+      const uint32_t ib = flags & 0xffu, codec = (flags >> 8) & 0xffu;
+      const uint32_t key_mode = (flags >> 16) & 0xffu, cls = flags >> 24;
       const bool scale = codec == FC_CODEC_DROPOUT_UNBIASED;     // fl32(fl64(g)/p), :60
       const bool generic = scale || (key_mode == FC_KEY_PHILOX && thresh != 0);
       auto fold = [&](uint32_t id, float v) {
@@ -523,7 +538,8 @@ __global__ __launch_bounds__(kSBlock, kSBlocksPerCU) void k_decode_sparse(Decode
           const float term = __fmul_rn(v, w);
           const float s2 = __fadd_rn(tile[loc], term);
           tile[loc] = s2;
-          if (__float_as_uint(s2) == 0x80000000u) cnt8[loc] = (uint8_t)(cnt8[loc] + 1u);
+          if (__float_as_uint(s2) == 0x80000000u && cls == 0u) cnt8[loc] = (uint8_t)(cnt8[loc] + 1u);
+          if (cls == 2u) cntC[loc] = (uint8_t)(cntC[loc] + 1u);
         } else {
           tile[loc] = v;
         }

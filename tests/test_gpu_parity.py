@@ -397,3 +397,73 @@ def test_fedavg_packets_dropout_unbiased_and_weights():
     np.testing.assert_array_equal(agg, ref)
     nz = ref != 0
     assert agg[nz].tobytes() == ref[nz].tobytes()
+
+
+def _signed_zero_grads(M, n, rng):
+    """Gradients built so that the FedAVG sum meets every sign-of-zero case: exact +-0
+    entries (kept at f = 0.5 as ties), negative denormals whose weighted term underflows
+    to -0, and columns where every row is -0."""
+    grads = []
+    for i in range(M):
+        x = (rng.standard_normal(n) * 1e-3).astype(np.float32)
+        sel = rng.uniform(size=n)
+        x[sel < 0.45] = -0.0
+        x[(sel >= 0.45) & (sel < 0.55)] = 0.0
+        x[(sel >= 0.55) & (sel < 0.65)] = -np.float32(1e-45)
+        # all-(-0) columns at the top indices: the tie rule keeps the highest indices of the
+        # zero-key group first, so every row keeps them and their sum stays -0
+        x[n - n // 16:] = -0.0
+        grads.append(x)
+    return grads
+
+
+@pytest.mark.parametrize("wkind", ["mean", "negative", "mixed_signs", "nonfinite"])
+def test_fedavg_packets_signed_zeros_and_weight_classes(wkind):
+    """k_decode_sparse skips the dropped coordinates; the dense sum of gar.py:44 adds
+    fl(+0 * w) there, which is +0 (w >= +0), -0 (w <= -0) or NaN (w = +-inf / NaN).  The
+    packet FedAVG must still equal the dense sum bit for bit (NaN positions for NaN)."""
+    codec = _codec()
+    M, n, f = 12, 20_011, 0.5
+    rng = np.random.default_rng({"mean": 1, "negative": 2, "mixed_signs": 3, "nonfinite": 4}[wkind])
+    grads = _signed_zero_grads(M, n, rng)
+    if wkind == "mean":
+        w = np.full(M, 1.0 / M, np.float32)
+    elif wkind == "negative":
+        w = -rng.uniform(0.01, 1, M).astype(np.float32)
+    elif wkind == "mixed_signs":
+        w = rng.uniform(-1, 1, M).astype(np.float32)
+        w[2], w[5] = np.float32(0.0), np.float32(-0.0)
+    else:
+        w = rng.uniform(0.01, 1, M).astype(np.float32)
+        w[3], w[7] = np.float32(np.inf), np.float32(np.nan)
+    k = co.num_kept(f, n)
+    pkts = [codec.encode_top(torch.from_numpy(x).cuda(), k) for x in grads]
+    agg = codec.decode_accumulate(pkts, list(w)).cpu().numpy()
+    rows = [co.compress({"compression_function": "top", "fraction_coordinate": f}, x)
+            for x in grads]
+    with np.errstate(invalid="ignore", over="ignore"):
+        ref = go.sequential_weighted_sum([r.astype(np.float32) for r in rows], w)
+    nan = np.isnan(ref)
+    np.testing.assert_array_equal(np.isnan(agg), nan)
+    assert agg[~nan].tobytes() == ref[~nan].tobytes()
+    if wkind == "mean":                         # the cases the -0 bookkeeping exists for
+        top = slice(n - n // 16, n)
+        assert np.signbit(ref[top]).all() and (ref[top] == 0).all()
+        negz = np.signbit(ref) & (ref == 0)
+        posz = ~np.signbit(ref) & (ref == 0)
+        assert negz.sum() >= n // 16 and posz[: n - n // 16].sum() > 100
+
+
+def test_fedavg_packets_signed_zeros_across_launches():
+    """> 64 packets: the sum continues across launches (acc_in), -0 bookkeeping included."""
+    codec = _codec()
+    M, n, f = 70, 9_001, 0.5
+    grads = _signed_zero_grads(M, n, np.random.default_rng(9))
+    w = np.full(M, 1.0 / M, np.float32)
+    k = co.num_kept(f, n)
+    pkts = [codec.encode_top(torch.from_numpy(x).cuda(), k) for x in grads]
+    agg = codec.decode_accumulate(pkts, list(w)).cpu().numpy()
+    rows = [co.compress({"compression_function": "top", "fraction_coordinate": f}, x)
+            for x in grads]
+    ref = go.sequential_weighted_sum([r.astype(np.float32) for r in rows], w)
+    assert agg.tobytes() == ref.tobytes()
