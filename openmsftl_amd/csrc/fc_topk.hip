@@ -499,13 +499,28 @@ __global__ __launch_bounds__(kCBlock, FC_COMPACT_WAVES_PER_EU) void k_compact(Co
 constexpr int kMGroups = 4 * kCWaves * 4;          // 128 groups of 64 elements
 constexpr int kMQ = 16;                            // groups per wave
 
-struct MagShared {
+// Workgroup barrier without a memory fence on the vector-memory counter: each wave's LDS
+// accesses are complete (lgkmcnt(0)) and the compiler may not move memory operations across
+// it.  __syncthreads() may also wait vmcnt(0), which would drain k_compact_dma's LDS-DMA
+// prefetch at every barrier.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+template <int STAGE, bool RAWBAR>
+struct MagSharedT {
+  static constexpr int kStageN = STAGE;
   uint32_t gcnt[kMGroups / 4];                     // 4 group counts (bytes, <= 64) per (i, w)
   uint32_t ncand[2];                               // candidates appended (by item parity)
   uint32_t pad_[2];
-  uint2 st[kStage + 4];                            // packed {chunk-local index, value bits}
-  uint16_t cbin[kStage + 2];
+  uint2 st[STAGE + 4];                             // packed {chunk-local index, value bits}
+  uint16_t cbin[STAGE + 2];
+  __device__ static void barrier() {
+    if (RAWBAR) lds_barrier();
+    else __syncthreads();
+  }
 };
+typedef MagSharedT<kStage, false> MagShared;
 
 // Block-uniform predicate parameters of one chunk.
 struct MagPred {
@@ -555,9 +570,9 @@ struct MagOut {
   uint32_t ib;
 };
 
-template <bool FAST>
+template <bool FAST, typename SH>
 __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred& P,
-                                                 float (&x)[kMQ], MagShared& sh,
+                                                 float (&x)[kMQ], SH& sh,
                                                  uint32_t chunk, uint32_t sbin, uint32_t par) {
   const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
   const uint32_t base = chunk * (uint32_t)kChunk;
@@ -577,7 +592,7 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
 #pragma unroll
     for (int i = 0; i < 4; ++i) sh.gcnt[i * kCWaves + w] = pk[i];
   }
-  __syncthreads();
+  SH::barrier();
   // recompute the predicates in phase 2 (one v_cmp each) instead of keeping 16 compare masks
   // live in SGPRs across the scan (that spilled 87 SGPRs)
 #pragma unroll
@@ -605,7 +620,7 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
 
   // ---- phase 2: listed entries -> LDS stage (or straight to the slot when dense) -----------
   const uint64_t slot = base;
-  if (tot_e <= (uint32_t)kStage) {                 // block-uniform
+  if (tot_e <= (uint32_t)SH::kStageN) {                 // block-uniform
 #pragma unroll
     for (int q = 0; q < kMQ; ++q) {
       const bool p = mag_listed<FAST>(P, x[q]);
@@ -639,14 +654,14 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
           const uint32_t key = mag_key(FAST ? x[q] : a.g[e]);
           if (cpos < (uint32_t)kCandSlot) a.cand[cslot + cpos] = comp_of(key, e, a.ib);
           const uint32_t bin = (key - P.t_lo) >> sbin;
-          if (cpos < (uint32_t)kStage) sh.cbin[cpos] = (uint16_t)bin;
+          if (cpos < (uint32_t)SH::kStageN) sh.cbin[cpos] = (uint16_t)bin;
           else atomicAdd(&a.chist[bin], 1u);
         }
       }
     }
   }
 #undef FC_LOC
-  __syncthreads();
+  SH::barrier();
   const uint32_t tot_c = sh.ncand[par];
   if (tid == 0) {
     TopkState* S = a.S;
@@ -655,7 +670,7 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
     atomicAdd(&S->shard_ent[chunk % kShards], tot_e);
     if (tot_c) atomicAdd(&S->shard_cnd[chunk % kShards], tot_c);
   }
-  if (tot_e <= (uint32_t)kStage) {                 // coalesced 16-B stores of the staged slot
+  if (tot_e <= (uint32_t)SH::kStageN) {                 // coalesced 16-B stores of the staged slot
     for (uint32_t t = 4 * tid; t < tot_e; t += 4 * kCBlock) {
       if (t + 4 <= tot_e) {
         const uint4 p0 = *reinterpret_cast<const uint4*>(&sh.st[t]);
@@ -671,7 +686,7 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
       }
     }
   }
-  const uint32_t nb = tot_c < (uint32_t)kStage ? tot_c : (uint32_t)kStage;
+  const uint32_t nb = tot_c < (uint32_t)SH::kStageN ? tot_c : (uint32_t)SH::kStageN;
   for (uint32_t t = tid; t < nb; t += kCBlock) atomicAdd(&a.chist[sh.cbin[t]], 1u);
 }
 
@@ -763,9 +778,10 @@ __device__ __forceinline__ void mag_load(const float* g, uint32_t chunk, uint64_
 // workgroups per CU overlap one another's load latency.  (A persistent variant that kept the
 // next item's loads in flight measured 1.3-2.5x SLOWER: hipcc spilled the second register set
 // and loop-carried state)
-__device__ __forceinline__ void compact_mag_item(const CompactArgs& a0, uint32_t client,
+template <typename SH>
+__device__ __forceinline__ void compact_mag_item(const CompactArgs& a0, const MagOut& o,
                                                  uint32_t chunk, const MagState& st,
-                                                 float (&x)[kMQ], MagShared& sh, uint32_t par) {
+                                                 float (&x)[kMQ], SH& sh, uint32_t par) {
   const int tid = threadIdx.x;
   const uint32_t base = chunk * (uint32_t)kChunk;
   const bool full = (uint64_t)base + kChunk <= a0.n;
@@ -783,11 +799,10 @@ __device__ __forceinline__ void compact_mag_item(const CompactArgs& a0, uint32_t
   // candidates: listed && key <= t_hi (t_hi >= the NaN key: every listed element)
   P.cand_all = P.t_hi >= 0x7f800001u;
   P.T_hi = __uint_as_float(P.cand_all ? 0x7f800000u : P.t_hi);
-  const MagOut o = mag_out(a0, client);
   if (fast) {
     compact_mag_body<true>(o, P, x, sh, chunk, st.sbin, par);
   } else if (none) {                                       // k = 0: nothing listed
-    __syncthreads();
+    SH::barrier();
     if (tid == 0) {
       o.cnt[chunk] = 0;
       o.ccnt[chunk] = 0;
@@ -808,7 +823,7 @@ __global__ __launch_bounds__(kCBlock, FC_MAG1_WAVES_PER_EU) void k_compact_mag1(
   mag_load(mag_g(a0, client), chunk, a0.n, x);             // g first, state behind it
   const MagState st = mag_state(mag_S(a0, client));
   if (threadIdx.x == 0) sh.ncand[0] = 0;
-  compact_mag_item(a0, client, chunk, st, x, sh, 0u);
+  compact_mag_item(a0, mag_out(a0, client), chunk, st, x, sh, 0u);
 }
 
 // --------------------------------------------------------------------------------------
