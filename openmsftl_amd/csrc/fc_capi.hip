@@ -147,8 +147,8 @@ static int launch_engine(int key_mode, const EngineArgs& base, int passes, hipSt
   return FC_OK;
 }
 
-// top-k compaction: k_compact_mag1, one workgroup per (chunk, client).  (A persistent
-// LDS-DMA variant measured 1.5x slower: DESIGN.md §Lessons.)
+// top-k compaction: k_compact_mag1, one workgroup per (chunk, client).  (Measured slower
+// and dropped: a persistent LDS-DMA ring, 1.5x; one wave per chunk, 1.1x — DESIGN.md §Lessons.)
 static void launch_compact_mag(const CompactArgs& a, uint32_t m, hipStream_t s) {
   hipLaunchKernelGGL(k_compact_mag1, dim3(a.nchunks, m), dim3(kCBlock), 0, s, a);
 }
