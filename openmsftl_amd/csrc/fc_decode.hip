@@ -482,27 +482,36 @@ __global__ __launch_bounds__(kSBlock, kSBlocksPerCU) void k_decode_sparse(Decode
   };
 
   // ---- item loads: counts one group ahead, entries clamped to the count -------------------
-  auto item_chunk = [&](uint32_t t) { return blockIdx.x + (t / M) * G; };
-  auto load_cnt = [&](uint32_t t) -> uint32_t {                  // uniform value, vector load
-    const uint32_t tt = t < T ? t : T - 1;
-    const SparseMeta& pm = s_meta[tt % M];
-    return ((gu32*)uni_ptr(pm.cnt))[item_chunk(tt)];
+  // Items are walked with incremental (chunk j, packet m) cursors (no per-item div/mod);
+  // past the end the cursor repeats the last item (loaded, ignored).
+  uint32_t cj = 0, cm = 0;                                       // next item to count-load
+  auto next_item = [&](uint32_t& m, uint32_t& c) {
+    const bool in = cj < J;
+    m = in ? cm : M - 1;
+    c = blockIdx.x + (in ? cj : J - 1) * G;
+    if (in && ++cm == M) { cm = 0; ++cj; }
   };
-  uint32_t cntg[kSGroup];
+  auto load_cnt = [&](uint32_t m, uint32_t c) -> uint32_t {     // uniform value, vector load
+    return ((gu32*)uni_ptr(s_meta[m].cnt))[c];
+  };
+  uint32_t gm[kSGroup], gc[kSGroup], cntg[kSGroup];
 #pragma unroll
-  for (int d = 0; d < kSGroup; ++d) cntg[d] = load_cnt((uint32_t)d);
+  for (int d = 0; d < kSGroup; ++d) {
+    next_item(gm[d], gc[d]);
+    cntg[d] = load_cnt(gm[d], gc[d]);
+  }
 
   init_tile(blockIdx.x);
   __syncthreads();
   for (uint32_t t0 = 0; t0 < T; t0 += kSGroup) {
     uint32_t ids[kSGroup][kSR];
     float vs[kSGroup][kSR];
-    uint32_t cn[kSGroup];
+    uint32_t cn[kSGroup], im[kSGroup], ic[kSGroup];
 #pragma unroll
     for (int d = 0; d < kSGroup; ++d) {
-      const uint32_t t = min(t0 + d, T - 1);                     // past the end: ignored
-      const SparseMeta& pm = s_meta[t % M];
-      const uint64_t lo = (uint64_t)item_chunk(t) * kChunk;
+      im[d] = gm[d]; ic[d] = gc[d];
+      const SparseMeta& pm = s_meta[im[d]];
+      const uint64_t lo = (uint64_t)ic[d] * kChunk;
       gf32* val = (gf32*)uni_ptr(pm.val) + lo;
       gu32* idx = (gu32*)uni_ptr(pm.idx) + lo;
       cn[d] = uni32(cntg[d]);
@@ -515,13 +524,16 @@ __global__ __launch_bounds__(kSBlock, kSBlocksPerCU) void k_decode_sparse(Decode
       }
     }
 #pragma unroll
-    for (int d = 0; d < kSGroup; ++d) cntg[d] = load_cnt(t0 + kSGroup + d);   // next group
+    for (int d = 0; d < kSGroup; ++d) {                          // next group's counts
+      next_item(gm[d], gc[d]);
+      cntg[d] = load_cnt(gm[d], gc[d]);
+    }
 #pragma unroll
     for (int d = 0; d < kSGroup; ++d) {
       const uint32_t t = t0 + d;
       if (t >= T) break;                                         // uniform
-      const uint32_t m = t % M;
-      const uint32_t c = item_chunk(t);
+      const uint32_t m = im[d];
+      const uint32_t c = ic[d];
       const uint64_t base = (uint64_t)c * kChunk;
       const SparseMeta pm = s_meta[m];
       const float w = __uint_as_float(uni32(__float_as_uint(pm.w)));

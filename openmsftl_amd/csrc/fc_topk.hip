@@ -501,8 +501,7 @@ constexpr int kMQ = 16;                            // groups per wave
 
 // Workgroup barrier without a memory fence on the vector-memory counter: each wave's LDS
 // accesses are complete (lgkmcnt(0)) and the compiler may not move memory operations across
-// it.  __syncthreads() may also wait vmcnt(0), which would drain k_compact_dma's LDS-DMA
-// prefetch at every barrier.
+// it (__syncthreads() may also wait vmcnt(0) and drain loads kept in flight across it).
 __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
