@@ -43,7 +43,7 @@ def parse():
     ap.add_argument("--no-single", action="store_true", help="skip the single-gradient probe")
     ap.add_argument("--no-batch", action="store_true",
                     help="encode client by client (fc_topk_encode) instead of batched")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_k_compact.json"),
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01_pmc_k_compact_mag1.json"),
                     help="PMC summary (profiles/) used for roofline.traffic")
     return ap.parse_args()
 
@@ -178,7 +178,7 @@ def main():
     alg_bytes = per_launch * (4.0 * n + 8.0 * k)
     achieved = alg_bytes / (t_compact_us * 1e-6) / 1e9
     pmc = load_pmc(args.pmc)
-    roofline = {"kernel": "fc::k_compact<0,0,0> (top-k encode pass, %d client(s) per launch)"
+    roofline = {"kernel": "fc::k_compact_mag1 (top-k encode pass, %d client(s) per launch)"
                           % per_launch, "bound": "hbm",
                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
@@ -189,7 +189,14 @@ def main():
                      "ms_per_step": round(kt.ms[c] / args.steps, 3)}
                  for c in L.TIME_CLASSES if kt.launches.get(c)}
 
-    extra = {"per_step_kernel_time": breakdown, "exact_fallbacks": redo_total[0]}
+    # whole step against the HBM roofline (SURVEY §8(d) batched FedAvg with fused
+    # decode-accumulate: M (4N + 16k) + 4N algorithmic bytes per GPU and step)
+    step_alg = M * (4.0 * n + 16.0 * k) + 4.0 * n
+    step_gbps = step_alg * world / (elapsed / args.steps) / 1e9
+    extra = {"per_step_kernel_time": breakdown, "exact_fallbacks": redo_total[0],
+             "step_roofline": {"alg_bytes_per_gpu": int(step_alg),
+                               "achieved_GBps": round(step_gbps, 1),
+                               "frac": round(step_gbps / world / HBM_PEAK_GBPS, 4)}}
     if rank == 0 and not args.no_single:
         extra["single_gradient"] = single_gradient(torch, codec, grads[0], k, n)
 

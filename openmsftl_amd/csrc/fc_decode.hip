@@ -381,7 +381,10 @@ __global__ __launch_bounds__(kDBlock, kDecBlocksPerCU) void k_decode(DecodeArgs 
 // --------------------------------------------------------------------------------------
 constexpr int kSBlock = 256;
 constexpr int kSR = 4;                         // entries per thread per item (1024 per item)
-constexpr int kSGroup = 4;                     // items whose loads are issued together
+#ifndef FC_SGROUP
+#define FC_SGROUP 4
+#endif
+constexpr int kSGroup = FC_SGROUP;             // items whose loads are issued together
 constexpr int kSBlocksPerCU = 3;               // 49 KB LDS per workgroup
 
 struct SparseMeta {
@@ -557,13 +560,32 @@ __global__ __launch_bounds__(kSBlock, kSBlocksPerCU) void k_decode_sparse(Decode
         }
       };
       if (!generic) {                                            // top-k / dropout-biased
+        // a packet's locations are distinct: all tile reads first, then all writes (one LDS
+        // round trip per item, not one per entry)
+        uint32_t loc[kSR];
+        bool ok[kSR];
+        float tv[kSR];
 #pragma unroll
         for (int r = 0; r < kSR; ++r) {
           const uint32_t e = (uint32_t)(tid + r * kSBlock);
           const uint32_t id = ids[d][r];
-          const float v = vs[d][r];
-          const bool keep = thresh == 0 || comp_of(mag_key(v), id, ib) >= thresh;
-          if (e < cn[d] && keep) fold(id, v);
+          const bool keep = thresh == 0 || comp_of(mag_key(vs[d][r]), id, ib) >= thresh;
+          loc[r] = id - (uint32_t)base;
+          ok[r] = e < cn[d] && keep && loc[r] < (uint32_t)kChunk;
+          tv[r] = 0.f;
+          if (ACC && ok[r]) tv[r] = tile[loc[r]];
+        }
+#pragma unroll
+        for (int r = 0; r < kSR; ++r) {
+          if (!ok[r]) continue;
+          if (ACC) {
+            const float s2 = __fadd_rn(tv[r], __fmul_rn(vs[d][r], w));
+            tile[loc[r]] = s2;
+            if (__float_as_uint(s2) == 0x80000000u && cls == 0u) cnt8[loc[r]] = (uint8_t)(cnt8[loc[r]] + 1u);
+            if (cls == 2u) cntC[loc[r]] = (uint8_t)(cntC[loc[r]] + 1u);
+          } else {
+            tile[loc[r]] = vs[d][r];
+          }
         }
       } else {
         const PktCache pk = meta_pkt_s(pm);

@@ -6,6 +6,8 @@ TAG=${1:-r01}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
+N=134217728
+K=13421773
 if [ -z "$SKIP_TESTS" ]; then
 echo "[gpu_round] tests"
 timeout -k 10 400 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread \
@@ -32,5 +34,11 @@ timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o pmc -- \
 echo "[gpu_round] pmc WRITE_SIZE"
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o pmc -- \
   python3 tools/kbench.py --iters 3 --batch 4 --tag pmc > $OUT/pmc_write.log 2>&1
+echo "[gpu_round] summaries"
+python3 tools/rocpd_summary.py stats $(find $OUT/prof_bench -name "*.db" | head -1) \
+  $OUT/kernel_stats_bench.csv
+python3 tools/rocpd_summary.py pmc $(find $OUT/pmc_fetch -name "*.db" | head -1) \
+  $(find $OUT/pmc_write -name "*.db" | head -1) k_compact_mag1 $OUT/pmc_k_compact_mag1.json \
+  --alg-bytes $((4 * (4 * N + 8 * K))) --clients-per-launch 4
 fi
 echo "[gpu_round] done"
