@@ -11,6 +11,9 @@
  *   Aggregator.aggregate_grads G build   aggregation.py:61-63   -> fc_decode_accumulate
  *   GAR.weighted_average / FedAvg        gar.py:32-46, 53-56    -> fc_decode_accumulate /
  *                                                                  fc_weighted_sum_dense
+ *   Aggregator.__merge_gradient          aggregation.py:80-93   -> fc_decode_accumulate /
+ *                                                                  fc_weighted_sum_dense (w=1)
+ *                                                                  + fc_div_scalar
  * The reference has no FFI of its own (100 % Python): these entry points are
  * what its Python layer binds through ctypes.
  *
@@ -179,6 +182,12 @@ int fc_decode_accumulate_continue(const fc_packet_view* views_dev, int m, int fo
  * pointers, w = DEVICE fp32[m]. */
 int fc_weighted_sum_dense(const float* const* rows, const float* w, int m, uint64_t n,
                           float* out, fc_stream_t stream);
+
+/* ---- hierarchical merge (aggregation.py:80-93): a cluster's mean
+ * np.mean(G[s:e, :], axis=0) is the +0-started row-order sum (fc_decode_accumulate /
+ * fc_weighted_sum_dense with weights 1.0) divided once by the row count: x = fl(x / d), in
+ * place, x a DEVICE fp32[n] (16-B aligned). */
+int fc_div_scalar(float* x, uint64_t n, float d, fc_stream_t stream);
 
 /* ---- measurement: HIP events around selected kernels, on the stream they run on -------
  * mask: FC_TIME_* bits.  Between fc_timing_begin and fc_timing_end every launch of a

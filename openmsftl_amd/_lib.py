@@ -83,6 +83,7 @@ SIGNATURES = {
     "fc_decode_accumulate": (_i32, [_vp, _i32, _i32, _u64, _vp, _vp]),
     "fc_decode_accumulate_continue": (_i32, [_vp, _i32, _i32, _u64, _vp, _vp]),
     "fc_weighted_sum_dense": (_i32, [_vp, _vp, _i32, _u64, _vp, _vp]),
+    "fc_div_scalar": (_i32, [_vp, _u64, ctypes.c_float, _vp]),
     "fc_timing_begin": (_i32, [ctypes.c_uint32]),
     "fc_timing_end": (_i32, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)]),
 }

@@ -356,3 +356,12 @@ def weighted_sum_dense(rows, weights: torch.Tensor, out: Optional[torch.Tensor] 
     L.check(lib.fc_weighted_sum_dense(_vp(ptrs), _vp(w), len(rows), n, _vp(out), _stream(dev)),
             "fc_weighted_sum_dense")
     return out
+
+
+def div_scalar(x: torch.Tensor, d: float) -> torch.Tensor:
+    """x = fl(x / d) in place (fp32 division; the count division of np.mean, aggregation.py:91)."""
+    lib = L.load()
+    _require_cuda_f32(x, "x")
+    L.check(lib.fc_div_scalar(_vp(x), x.numel(), ctypes.c_float(d), _stream(x.device)),
+            "fc_div_scalar")
+    return x

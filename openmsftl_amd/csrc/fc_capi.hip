@@ -466,6 +466,19 @@ int fc_decode_accumulate_continue(const fc_packet_view* views_dev, int m, int fo
   return decode_accumulate(views_dev, m, format, n, acc, true, stream);
 }
 
+int fc_div_scalar(float* x, uint64_t n, float d, fc_stream_t stream) {
+  FC_CHECK(x != nullptr, "x is NULL");
+  FC_CHECK(n >= 1, "n=0");
+  FC_CHECK(((uintptr_t)x & 15) == 0, "x must be 16-byte aligned");
+  uint64_t blocks = (n / 4 + kBlock - 1) / kBlock;
+  if (blocks < 1) blocks = 1;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(k_div_scalar, dim3((uint32_t)blocks), dim3(kBlock), 0, (hipStream_t)stream,
+                     x, n, d);
+  FC_LAUNCHED("k_div_scalar");
+  return FC_OK;
+}
+
 int fc_weighted_sum_dense(const float* const* rows, const float* w, int m, uint64_t n,
                           float* out, fc_stream_t stream) {
   FC_CHECK(rows && w && out, "NULL argument");

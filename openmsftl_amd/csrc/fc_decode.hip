@@ -9,7 +9,8 @@
 // then each lane owns the same (i, w, lane, j) element layout as the encoder and either
 // writes the dense result (ACC = false; compression.py:33-37 / 52 / 60) or folds it into a
 // register accumulator exactly as gar.py:44 does on the dense G:
-//   acc = fl(w_0 * d_0);  acc = fl(acc + fl(w_i * d_i))   (no FMA: __fmul_rn / __fadd_rn)
+//   acc = +0;  acc = fl(acc + fl(w_i * d_i))  for i in row order  (no FMA: __fmul_rn /
+//   __fadd_rn; NumPy's axis-0 add.reduce starts from +0, so the sum is never -0)
 // so the FedAVG of M packets reads each packet once and writes the aggregate once.
 #include <type_traits>
 
@@ -334,9 +335,9 @@ __global__ __launch_bounds__(kDBlock, kDecBlocksPerCU) void k_decode(DecodeArgs 
           if (ACC) {
             const float4 cw = make_float4(__fmul_rn(dv.x, pk.w), __fmul_rn(dv.y, pk.w),
                                           __fmul_rn(dv.z, pk.w), __fmul_rn(dv.w, pk.w));
-            if (m == 0 && !a.acc_in) acc[i] = cw;
-            else acc[i] = make_float4(__fadd_rn(acc[i].x, cw.x), __fadd_rn(acc[i].y, cw.y),
-                                      __fadd_rn(acc[i].z, cw.z), __fadd_rn(acc[i].w, cw.w));
+            if (m == 0 && !a.acc_in) acc[i] = make_float4(0.f, 0.f, 0.f, 0.f);   // np.sum: +0 start
+            acc[i] = make_float4(__fadd_rn(acc[i].x, cw.x), __fadd_rn(acc[i].y, cw.y),
+                                 __fadd_rn(acc[i].z, cw.z), __fadd_rn(acc[i].w, cw.w));
           } else {
             store_out(reinterpret_cast<float*>(a.out), eo, a.n, dv);   // single packet: done
           }
@@ -363,17 +364,14 @@ __global__ __launch_bounds__(kDBlock, kDecBlocksPerCU) void k_decode(DecodeArgs 
 // so the work per packet is proportional to its entries (k), not to N: k_decode<ACC> folded
 // all 8192 elements of the chunk per packet and was VALU/LDS-bound at ~38 us per 128 M packet.
 //
-// A dropped coordinate of packet i adds the term d_i = fl(dz * w_i) (dz = +0, the dropped
-// value; NaN for dropout-unbiased with p == 0).  Skipping it is exact unless:
-//   class A, d_i == +0 (w_i >= +0): x + (+0) == x for every x but -0.  A running sum can only
-//     BE -0 while every term so far was -0 (nonzero terms never cancel to -0 under RN, and
-//     +0 + -0 == +0), so the tile starts at -0 (the additive identity: -0 + t == t) and, while
-//     an element's sum is -0, counts its class-A folds (cnt8, rare path).  At write-out a -0
-//     that some class-A packet did not fold becomes +0.
-//   class B, d_i == -0 (w_i <= -0): neutral for every x.
-//   class C, d_i == NaN (w_i = +-inf / NaN, or p == 0): every element the packet did not fold
-//     is NaN; counted by cntC.
-// The result is exactly the dense sum of gar.py:44 over G.
+// gar.py:44 is np.sum(G * w[:, None], axis=0): NumPy's axis-0 add.reduce starts from +0 and
+// adds the rows in order (probed: tests/test_oracle_golden.py::test_numpy_axis0_sum_order),
+// so the dense sum is s = fl(...fl(fl(+0 + t_0) + t_1)...).  Such a sum is never -0 (+0 + -0
+// == +0, and nonzero terms never cancel to -0 under RN), so skipping a dropped coordinate's
+// term d_i = fl(dz * w_i) is exact whenever d_i is +-0: the tile starts at +0 and only kept
+// entries are folded.  The exception is d_i == NaN (w_i = +-inf / NaN, or dropout-unbiased
+// with p == 0, where dz = 0/0): every element such a "poisoning" packet did not fold is NaN
+// (cntC counts their folds).  The result is exactly the dense sum of gar.py:44 over G.
 //
 // Loads: every item (packet, chunk) reads its first 1024 slot entries with addresses clamped
 // to the slot's count (lanes past it re-read entry 0: no extra HBM traffic, no divergent
@@ -385,7 +383,7 @@ constexpr int kSR = 4;                         // entries per thread per item (1
 #define FC_SGROUP 4
 #endif
 constexpr int kSGroup = FC_SGROUP;             // items whose loads are issued together
-constexpr int kSBlocksPerCU = 3;               // 49 KB LDS per workgroup
+constexpr int kSBlocksPerCU = 3;               // 41 KB LDS per workgroup
 
 struct SparseMeta {
   const uint32_t* idx;
@@ -410,10 +408,9 @@ __device__ __forceinline__ PktCache meta_pkt_s(const SparseMeta& pm) {
 template <bool ACC>
 __global__ __launch_bounds__(kSBlock, kSBlocksPerCU) void k_decode_sparse(DecodeArgs a) {
   __shared__ __attribute__((aligned(16))) float tile[kChunk];
-  __shared__ __attribute__((aligned(16))) uint8_t cnt8[ACC ? kChunk : 16];   // class-A folds at -0
-  __shared__ __attribute__((aligned(16))) uint8_t cntC[ACC ? kChunk : 16];   // class-C folds
+  __shared__ __attribute__((aligned(16))) uint8_t cntC[ACC ? kChunk : 16];   // poisoning folds
   __shared__ SparseMeta s_meta[ACC ? kDecMaxM : 1];
-  __shared__ uint32_t s_nA, s_nC;
+  __shared__ uint32_t s_nC;
   const int tid = threadIdx.x;
   const uint32_t M = ACC ? (uint32_t)a.m : 1u;
   const uint32_t nch = (uint32_t)((a.n + kChunk - 1) / kChunk);
@@ -422,7 +419,7 @@ __global__ __launch_bounds__(kSBlock, kSBlocksPerCU) void k_decode_sparse(Decode
   const uint32_t J = (nch - blockIdx.x + G - 1) / G;             // chunks of this workgroup
   const uint32_t T = J * M;                                      // items (chunk-major)
 
-  if (tid == 0) { s_nA = 0; s_nC = 0; }
+  if (tid == 0) s_nC = 0;
   __syncthreads();
   if (tid < (int)M) {
     const fc_packet_view v = ACC ? a.views[tid] : a.one;
@@ -432,22 +429,20 @@ __global__ __launch_bounds__(kSBlock, kSBlocksPerCU) void k_decode_sparse(Decode
     d.seed = h->seed; d.offset = h->offset; d.p = h->p;
     d.thresh = h->thresh; d.w = v.weight;
     d.flags = (h->index_bits & 0xffu) | ((h->codec & 0xffu) << 8) | (h->key_mode << 16);
-    // class of the packet's dropped term fl(dz * w): A +0, B -0, C NaN (bits 24-25)
+    // a packet whose dropped term fl(dz * w) is NaN poisons what it does not fold (bit 24)
     const float dz = (h->codec == FC_CODEC_DROPOUT_UNBIASED && h->p == 0.0) ? __uint_as_float(0x7fc00000u) : 0.0f;
-    const uint32_t td = __float_as_uint(__fmul_rn(dz, v.weight));
-    const uint32_t cls = td == 0u ? 0u : td == 0x80000000u ? 1u : 2u;
-    d.flags |= cls << 24;
+    const bool poison = __fmul_rn(dz, v.weight) != __fmul_rn(dz, v.weight);
+    d.flags |= (uint32_t)poison << 24;
     s_meta[tid] = d;
-    if (cls == 0u) atomicAdd(&s_nA, 1u);
-    if (cls == 2u) atomicAdd(&s_nC, 1u);
+    if (poison) atomicAdd(&s_nC, 1u);
   }
   __syncthreads();
-  const uint32_t nA = s_nA, nC = s_nC;
+  const uint32_t nC = s_nC;
 
   // ---- per-chunk tile init / write-out (each thread owns elements tid*4 + i*1024) ----------
   auto init_tile = [&](uint32_t c) {
     const uint64_t base = (uint64_t)c * kChunk;
-    float dz = -0.0f;                                            // identity of the fold
+    float dz = 0.0f;                                             // np.sum's +0 start
     if (!ACC) dz = dropped_f32(meta_pkt_s(s_meta[0]));
 #pragma unroll
     for (int i = 0; i < kChunk / (kSBlock * 4); ++i) {
@@ -455,10 +450,7 @@ __global__ __launch_bounds__(kSBlock, kSBlocksPerCU) void k_decode_sparse(Decode
       float4 v = make_float4(dz, dz, dz, dz);
       if (ACC && a.acc_in) v = load4(reinterpret_cast<const float*>(a.out), base + loc, a.n);
       *reinterpret_cast<float4*>(&tile[loc]) = v;
-      if (ACC) {
-        *reinterpret_cast<uint32_t*>(&cnt8[loc]) = 0u;
-        if (nC) *reinterpret_cast<uint32_t*>(&cntC[loc]) = 0u;
-      }
+      if (ACC && nC) *reinterpret_cast<uint32_t*>(&cntC[loc]) = 0u;
     }
   };
   auto write_tile = [&](uint32_t c) {
@@ -468,17 +460,11 @@ __global__ __launch_bounds__(kSBlock, kSBlocksPerCU) void k_decode_sparse(Decode
     for (int i = 0; i < kChunk / (kSBlock * 4); ++i) {
       const uint32_t loc = (uint32_t)(i * 1024 + tid * 4);
       float4 v = *reinterpret_cast<const float4*>(&tile[loc]);
-      if (ACC) {
-        const uint32_t c4 = *reinterpret_cast<const uint32_t*>(&cnt8[loc]);
-        const uint32_t k4 = nC ? *reinterpret_cast<const uint32_t*>(&cntC[loc]) : 0u;
-        // -0 that some class-A packet did not fold: the dense sum added +0 there; an element
-        // some class-C packet did not fold: the dense sum added NaN there
-        auto fix = [&](float x, uint32_t cn, uint32_t kc) {
-          if (kc < nC) return __uint_as_float(0x7fc00000u);
-          return (__float_as_uint(x) == 0x80000000u && cn < nA) ? 0.0f : x;
-        };
-        v = make_float4(fix(v.x, c4 & 0xffu, k4 & 0xffu), fix(v.y, (c4 >> 8) & 0xffu, (k4 >> 8) & 0xffu),
-                        fix(v.z, (c4 >> 16) & 0xffu, (k4 >> 16) & 0xffu), fix(v.w, c4 >> 24, k4 >> 24));
+      if (ACC && nC) {                                           // poisoning packets
+        const uint32_t k4 = *reinterpret_cast<const uint32_t*>(&cntC[loc]);
+        auto fix = [&](float x, uint32_t kc) { return kc < nC ? __uint_as_float(0x7fc00000u) : x; };
+        v = make_float4(fix(v.x, k4 & 0xffu), fix(v.y, (k4 >> 8) & 0xffu),
+                        fix(v.z, (k4 >> 16) & 0xffu), fix(v.w, k4 >> 24));
       }
       store_out(out, base + loc, a.n, v);
     }
@@ -543,7 +529,7 @@ __global__ __launch_bounds__(kSBlock, kSBlocksPerCU) void k_decode_sparse(Decode
       const uint64_t thresh = uni64(pm.thresh);
       const uint32_t flags = uni32(pm.flags);
       const uint32_t ib = flags & 0xffu, codec = (flags >> 8) & 0xffu;
-      const uint32_t key_mode = (flags >> 16) & 0xffu, cls = flags >> 24;
+      const uint32_t key_mode = (flags >> 16) & 0xffu, poison = flags >> 24;
       const bool scale = codec == FC_CODEC_DROPOUT_UNBIASED;     // fl32(fl64(g)/p), :60
       const bool generic = scale || (key_mode == FC_KEY_PHILOX && thresh != 0);
       auto fold = [&](uint32_t id, float v) {
@@ -553,8 +539,7 @@ __global__ __launch_bounds__(kSBlock, kSBlocksPerCU) void k_decode_sparse(Decode
           const float term = __fmul_rn(v, w);
           const float s2 = __fadd_rn(tile[loc], term);
           tile[loc] = s2;
-          if (__float_as_uint(s2) == 0x80000000u && cls == 0u) cnt8[loc] = (uint8_t)(cnt8[loc] + 1u);
-          if (cls == 2u) cntC[loc] = (uint8_t)(cntC[loc] + 1u);
+          if (poison) cntC[loc] = (uint8_t)(cntC[loc] + 1u);
         } else {
           tile[loc] = v;
         }
@@ -581,8 +566,7 @@ __global__ __launch_bounds__(kSBlock, kSBlocksPerCU) void k_decode_sparse(Decode
           if (ACC) {
             const float s2 = __fadd_rn(tv[r], __fmul_rn(vs[d][r], w));
             tile[loc[r]] = s2;
-            if (__float_as_uint(s2) == 0x80000000u && cls == 0u) cnt8[loc[r]] = (uint8_t)(cnt8[loc[r]] + 1u);
-            if (cls == 2u) cntC[loc[r]] = (uint8_t)(cntC[loc[r]] + 1u);
+            if (poison) cntC[loc[r]] = (uint8_t)(cntC[loc[r]] + 1u);
           } else {
             tile[loc[r]] = vs[d][r];
           }
@@ -643,11 +627,25 @@ __global__ __launch_bounds__(kBlock) void k_wsum(const float* const* rows, const
       const float wr = w[r];
       const float4 cw = make_float4(__fmul_rn(x.x, wr), __fmul_rn(x.y, wr),
                                     __fmul_rn(x.z, wr), __fmul_rn(x.w, wr));
-      if (r == 0) acc = cw;
-      else acc = make_float4(__fadd_rn(acc.x, cw.x), __fadd_rn(acc.y, cw.y),
-                             __fadd_rn(acc.z, cw.z), __fadd_rn(acc.w, cw.w));
+      acc = make_float4(__fadd_rn(acc.x, cw.x), __fadd_rn(acc.y, cw.y),      // from +0 (np.sum)
+                        __fadd_rn(acc.z, cw.z), __fadd_rn(acc.w, cw.w));
     }
     store_out(out, e, n, acc);
+  }
+}
+
+// Cluster mean (aggregation.py:91 np.mean(G[s:e], axis=0)): x = fl(x / d) in place, x the
+// +0-started row-order sum of the cluster (k_decode_sparse / k_wsum with weights 1).
+__global__ __launch_bounds__(kBlock) void k_div_scalar(float* x, uint64_t n, float d) {
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock * 4;
+  for (uint64_t e = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) * 4; e < n; e += stride) {
+    if (e + 4 <= n) {
+      float4 v = *reinterpret_cast<float4*>(x + e);
+      v = make_float4(__fdiv_rn(v.x, d), __fdiv_rn(v.y, d), __fdiv_rn(v.z, d), __fdiv_rn(v.w, d));
+      *reinterpret_cast<float4*>(x + e) = v;
+    } else {
+      for (uint64_t i = e; i < n; ++i) x[i] = __fdiv_rn(x[i], d);
+    }
   }
 }
 

@@ -33,13 +33,36 @@ class FedAvgOracle:
 
 def sequential_weighted_sum(rows, weights) -> np.ndarray:
     """The exact arithmetic of gar.py:44 for an (M,N) fp32 G, spelled out:
-    ``acc = fl(w0*g0); acc = fl(acc + fl(wi*gi))`` in row order (probed
-    bit-equal to np.sum(axis=0) for M=4,10,128)."""
+    ``acc = +0; acc = fl(acc + fl(wi*gi))`` in row order.  NumPy's axis-0 ``add.reduce``
+    starts from the additive identity +0 (not from row 0): the two differ only in the sign
+    of zero (an all-(-0) column sums to +0), pinned by
+    tests/test_oracle_golden.py::test_numpy_axis0_sum_order (SURVEY.md §0.6 probed the
+    nonzero values bit-equal for M=4,10,128)."""
     acc = None
     for w, r in zip(weights, rows):
         c = np.multiply(r, w)
-        acc = c.copy() if acc is None else np.add(acc, c)
+        acc = np.add(np.zeros_like(c), c) if acc is None else np.add(acc, c)
     return acc
+
+
+def cluster_mean(G: np.ndarray, start: int, stop: int) -> np.ndarray:
+    """aggregation.py:91 ``np.mean(G[s:e, :], axis=0)`` for fp32 G, spelled out: the +0-started
+    row-order sum, then one fp32 division by the row count (probed equal to np.mean)."""
+    acc = np.zeros(G.shape[1], dtype=G.dtype)
+    for r in range(start, stop):
+        acc = np.add(acc, G[r])
+    return np.true_divide(acc, G.dtype.type(stop - start))
+
+
+def merge_gradient(G: np.ndarray, cluster_size: int) -> np.ndarray:
+    """aggregation.py:80-93 (``Aggregator.__merge_gradient``): rows averaged over consecutive
+    clusters of ``cluster_size``; the last cluster absorbs the remainder."""
+    num = G.shape[0] // cluster_size
+    assert num > 0, "Too small cluter size: {} // {} == 0".format(G.shape[0], cluster_size)
+    bounds = [[i * cluster_size, (i + 1) * cluster_size] for i in range(num)]
+    if bounds[-1][1] < G.shape[0]:
+        bounds[-1][1] = G.shape[0]
+    return np.stack([cluster_mean(G, s, e) for s, e in bounds]).astype(G.dtype)
 
 
 def build_dense_G(compressed_rows, dtype) -> np.ndarray:

@@ -58,3 +58,31 @@ def has_tie_at_boundary(g: np.ndarray, k: int) -> bool:
         return False
     keys = np.sort(mag_key(g))[::-1]          # NaN is one key, above +inf
     return bool(keys[k - 1] == keys[k])
+
+
+class AggGolden:
+    """tests/golden/make_golden_agg.py: FedAvg sign-of-zero and hierarchical-merge cases."""
+
+    def __init__(self):
+        with open(os.path.join(GOLDEN_DIR, "manifest_agg.json")) as fh:
+            self.manifest = json.load(fh)
+        self.arrays = np.load(os.path.join(GOLDEN_DIR, "golden_agg.npz"))
+
+    def cases(self, prefix=""):
+        return sorted(k for k in self.manifest["cases"] if k.startswith(prefix))
+
+    def meta(self, name):
+        return self.manifest["cases"][name]
+
+    def arr(self, name, key):
+        return self.arrays[f"{name}|{key}"]
+
+
+_AGG = None
+
+
+def agg_golden() -> AggGolden:
+    global _AGG
+    if _AGG is None:
+        _AGG = AggGolden()
+    return _AGG

@@ -147,3 +147,44 @@ def test_philox_known_answers():
     for ctr, key, want in KAT:
         got = philox4x32_10(*[np.uint32(c) for c in ctr], *[np.uint32(k) for k in key])
         assert tuple(int(x) for x in got) == want
+
+
+# ---- aggregation rows (tests/golden/make_golden_agg.py: the reference's own outputs) ------
+from conftest import agg_golden  # noqa: E402
+
+A = agg_golden()
+
+
+def test_numpy_axis0_sum_order():
+    """gar.py:44's np.sum(axis=0) = row-order fp32 adds starting from +0: an all-(-0) column
+    sums to +0, a one-row G too; nonzero values equal the plain left-to-right chain."""
+    rng = np.random.default_rng(5)
+    for M in (1, 2, 7, 64):
+        Gm = (rng.standard_normal((M, 999)) * 10.0 ** rng.uniform(-6, 3, (M, 1))).astype(np.float32)
+        Gm[:, :50] = -0.0
+        Gm[:, 50:60] = -np.float32(1e-45)
+        w = np.full(M, 1.0 / M, np.float32)
+        ref = np.sum(np.multiply(Gm, w[:, None]), axis=0)
+        assert go.sequential_weighted_sum(list(Gm), w).tobytes() == ref.tobytes()
+        assert not np.signbit(ref[:50]).any()
+
+
+@pytest.mark.parametrize("name", A.cases("fedavg_signed__"))
+def test_fedavg_signed_zero_matches_reference(name):
+    Gm, ref = A.arr(name, "G"), A.arr(name, "output")
+    w = np.full(Gm.shape[0], 1.0 / Gm.shape[0], dtype=np.float32)
+    assert go.sequential_weighted_sum(list(Gm), w).tobytes() == ref.tobytes()
+    assert go.FedAvgOracle({}).aggregate(Gm).tobytes() == ref.tobytes()
+
+
+@pytest.mark.parametrize("name", A.cases("hier__"))
+def test_hierarchical_merge_matches_reference(name):
+    """aggregation.py:68-75 / 80-93: cluster means (last cluster absorbs the remainder), then
+    FedAvg over the merged rows."""
+    Gm, sizes = A.arr(name, "G"), A.meta(name)["cluster_size_list"]
+    H = Gm
+    for cs in sizes:
+        H = go.merge_gradient(H, cs)
+    assert H.tobytes() == A.arr(name, "merged").tobytes()
+    out = go.FedAvgOracle({}).aggregate(H)
+    assert out.tobytes() == A.arr(name, "output").tobytes()

@@ -1,5 +1,4 @@
 set -e
-timeout -k 10 300 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/t.log 2>&1 || { tail -40 gpurun_out/t.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/t.log 2>&1 || { tail -60 gpurun_out/t.log; exit 1; }
 tail -1 gpurun_out/t.log
 timeout -k 10 120 python tools/kbench.py --iters 5 --tag single
-timeout -k 10 120 python tools/kbench.py --iters 5 --f 0.01 --tag single_f01
