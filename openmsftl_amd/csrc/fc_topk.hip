@@ -497,7 +497,13 @@ __global__ __launch_bounds__(kCBlock, FC_COMPACT_WAVES_PER_EU) void k_compact(Co
 // Candidates (rare) are appended through an LDS counter: k_resolve does not need them ordered.
 // --------------------------------------------------------------------------------------
 constexpr int kMGroups = 4 * kCWaves * 4;          // 128 groups of 64 elements
-constexpr int kMQ = 16;                            // groups per wave
+constexpr int kMQ = 16;                            // groups per wave (512-thread workgroups)
+// elements per lane for NW waves per chunk; chunk-element stride of the i index
+template <int NW> struct MagGeo {
+  static constexpr int kQ = kChunk / (NW * 64);    // 16 (NW = 8) or 32 (NW = 4)
+  static constexpr int kIStride = NW * 256;        // e = i*kIStride + w*256 + j*64 + lane
+  static constexpr int kThreads = NW * 64;
+};
 
 // Workgroup barrier without a memory fence on the vector-memory counter: each wave's LDS
 // accesses are complete (lgkmcnt(0)) and the compiler may not move memory operations across
@@ -543,10 +549,12 @@ __device__ __forceinline__ bool mag_cand(const MagPred& P, float v) {
 }
 // k_compact's exact integer predicates (listed: comp >= L64; candidate: key in [t_lo, t_hi])
 // for element e0 + offset(q), written over x[q].
-__device__ __forceinline__ void mag_exact_bits(const MagPred& P, float (&x)[16], uint32_t e0) {
+template <int NW>
+__device__ __forceinline__ void mag_exact_bits(const MagPred& P, float (&x)[MagGeo<NW>::kQ],
+                                               uint32_t e0) {
 #pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const uint32_t e = e0 + (q >> 2) * 2048 + (q & 3) * 64;
+  for (int q = 0; q < MagGeo<NW>::kQ; ++q) {
+    const uint32_t e = e0 + (q >> 2) * MagGeo<NW>::kIStride + (q & 3) * 64;
     const uint32_t key = mag_key(x[q]);
     const bool valid = e < P.n32;
     const bool p = valid & ((key > P.Lk) | ((key == P.Lk) & (e >= P.Li)));
@@ -569,18 +577,19 @@ struct MagOut {
   uint32_t ib;
 };
 
-template <bool FAST, typename SH>
+template <bool FAST, typename SH, int NW>
 __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred& P,
-                                                 float (&x)[kMQ], SH& sh,
+                                                 float (&x)[MagGeo<NW>::kQ], SH& sh,
                                                  uint32_t chunk, uint32_t sbin, uint32_t par) {
   const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
   const uint32_t base = chunk * (uint32_t)kChunk;
   const uint32_t lbase = (uint32_t)(w * 256 + lane);
-#define FC_LOC(q) (lbase + ((q) >> 2) * 2048 + ((q) & 3) * 64)
+  constexpr int NQ = MagGeo<NW>::kQ, NI = NQ / 4;
+#define FC_LOC(q) (lbase + ((q) >> 2) * MagGeo<NW>::kIStride + ((q) & 3) * 64)
   // ---- phase 1: group counts (scalar popcounts of the compare masks) ---------------------
-  uint32_t pk[4];
+  uint32_t pk[NI];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < NI; ++i) {
     pk[i] = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
@@ -589,13 +598,13 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
   }
   if (lane == 0) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) sh.gcnt[i * kCWaves + w] = pk[i];
+    for (int i = 0; i < NI; ++i) sh.gcnt[i * NW + w] = pk[i];
   }
   SH::barrier();
   // recompute the predicates in phase 2 (one v_cmp each) instead of keeping 16 compare masks
   // live in SGPRs across the scan (that spilled 87 SGPRs)
 #pragma unroll
-  for (int q = 0; q < kMQ; ++q) asm volatile("" : "+v"(x[q]));
+  for (int q = 0; q < NQ; ++q) asm volatile("" : "+v"(x[q]));
   // the other parity's counter was last read before this item's barrier: reset it for the next
   if (tid == 0) sh.ncand[par ^ 1u] = 0;
   // every wave scans the 32 packed (i, w) words itself (no second barrier): lane L < 32 holds
@@ -608,29 +617,27 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
   const uint32_t e1 = e0 + (word & 0xffu), e2 = e1 + ((word >> 8) & 0xffu);
   const uint32_t e3 = e2 + ((word >> 16) & 0xffu);
   const uint32_t o01 = e0 | (e1 << 16), o23 = e2 | (e3 << 16);
-  uint32_t goff[kMQ];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const uint32_t a01 = (uint32_t)__builtin_amdgcn_readlane((int)o01, i * kCWaves + w);
-    const uint32_t a23 = (uint32_t)__builtin_amdgcn_readlane((int)o23, i * kCWaves + w);
-    goff[i * 4 + 0] = a01 & 0xffffu; goff[i * 4 + 1] = a01 >> 16;
-    goff[i * 4 + 2] = a23 & 0xffffu; goff[i * 4 + 3] = a23 >> 16;
-  }
+  // group q's slot offset, read from its holder lane where it is used (a precomputed array
+  // is NQ live SGPRs: it spilled at NQ = 32)
+  auto goff_of = [&](int q) -> uint32_t {
+    const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)((q & 2) ? o23 : o01), (q >> 2) * NW + w);
+    return (q & 1) ? v >> 16 : v & 0xffffu;
+  };
 
   // ---- phase 2: listed entries -> LDS stage (or straight to the slot when dense) -----------
   const uint64_t slot = base;
   if (tot_e <= (uint32_t)SH::kStageN) {                 // block-uniform
 #pragma unroll
-    for (int q = 0; q < kMQ; ++q) {
+    for (int q = 0; q < NQ; ++q) {
       const bool p = mag_listed<FAST>(P, x[q]);
-      const uint32_t pos = prefix_count(__ballot(p)) + goff[q];
+      const uint32_t pos = prefix_count(__ballot(p)) + goff_of(q);
       if (p) sh.st[pos] = make_uint2(FC_LOC(q), __float_as_uint(FAST ? x[q] : a.g[base + FC_LOC(q)]));
     }
   } else {
 #pragma unroll
-    for (int q = 0; q < kMQ; ++q) {
+    for (int q = 0; q < NQ; ++q) {
       const bool p = mag_listed<FAST>(P, x[q]);
-      const uint32_t pos = prefix_count(__ballot(p)) + goff[q];
+      const uint32_t pos = prefix_count(__ballot(p)) + goff_of(q);
       if (p) {
         a.idx[slot + pos] = base + FC_LOC(q);
         a.val[slot + pos] = FAST ? x[q] : a.g[base + FC_LOC(q)];
@@ -641,7 +648,7 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
   if (P.cand_on) {
     const uint64_t cslot = (uint64_t)chunk * kCandSlot;
 #pragma unroll
-    for (int q = 0; q < kMQ; ++q) {
+    for (int q = 0; q < NQ; ++q) {
       const bool c = mag_cand<FAST>(P, x[q]);
       const uint64_t mc = __ballot(c);
       if (mc) {                                    // wave-uniform
@@ -670,7 +677,7 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
     if (tot_c) atomicAdd(&S->shard_cnd[chunk % kShards], tot_c);
   }
   if (tot_e <= (uint32_t)SH::kStageN) {                 // coalesced 16-B stores of the staged slot
-    for (uint32_t t = 4 * tid; t < tot_e; t += 4 * kCBlock) {
+    for (uint32_t t = 4 * tid; t < tot_e; t += 4 * MagGeo<NW>::kThreads) {
       if (t + 4 <= tot_e) {
         const uint4 p0 = *reinterpret_cast<const uint4*>(&sh.st[t]);
         const uint4 p1 = *reinterpret_cast<const uint4*>(&sh.st[t + 2]);
@@ -686,7 +693,7 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
     }
   }
   const uint32_t nb = tot_c < (uint32_t)SH::kStageN ? tot_c : (uint32_t)SH::kStageN;
-  for (uint32_t t = tid; t < nb; t += kCBlock) atomicAdd(&a.chist[sh.cbin[t]], 1u);
+  for (uint32_t t = tid; t < nb; t += MagGeo<NW>::kThreads) atomicAdd(&a.chist[sh.cbin[t]], 1u);
 }
 
 // Per-client records (job table, encoder state) are read with SCALAR loads: no kernel of this
@@ -756,31 +763,33 @@ __device__ __forceinline__ MagState mag_state(const TopkState* S) {
 
 // The chunk's 16 elements per lane in the ballot layout: whole chunk = nt loads; the last,
 // partial chunk clamps its addresses (its values past n are never listed: exact path).
+template <int NW>
 __device__ __forceinline__ void mag_load(const float* g, uint32_t chunk, uint64_t n,
-                                         float (&x)[kMQ]) {
+                                         float (&x)[MagGeo<NW>::kQ]) {
+  constexpr int NQ = MagGeo<NW>::kQ, IS = MagGeo<NW>::kIStride;
   const uint32_t base = chunk * (uint32_t)kChunk;
   typedef __attribute__((address_space(1))) const float gf;
   const uint32_t l0 = (uint32_t)((threadIdx.x >> 6) * 256 + lane_id());
   if ((uint64_t)base + kChunk > n) {
     const uint32_t last = (uint32_t)(n - 1) - base;
 #pragma unroll
-    for (int q = 0; q < kMQ; ++q)
-      x[q] = ((gf*)g)[base + min(l0 + (q >> 2) * 2048 + (q & 3) * 64, last)];
+    for (int q = 0; q < NQ; ++q)
+      x[q] = ((gf*)g)[base + min(l0 + (q >> 2) * IS + (q & 3) * 64, last)];
     return;
   }
   gf* gp = (gf*)g + base + l0;
 #pragma unroll
-  for (int q = 0; q < kMQ; ++q) x[q] = __builtin_nontemporal_load(gp + (q >> 2) * 2048 + (q & 3) * 64);
+  for (int q = 0; q < NQ; ++q) x[q] = __builtin_nontemporal_load(gp + (q >> 2) * IS + (q & 3) * 64);
 }
 
 // One workgroup per item (grid = (nchunks, clients)); <= 64 VGPRs, so 4 resident 512-thread
 // workgroups per CU overlap one another's load latency.  (A persistent variant that kept the
 // next item's loads in flight measured 1.3-2.5x SLOWER: hipcc spilled the second register set
 // and loop-carried state)
-template <typename SH>
+template <int NW, typename SH>
 __device__ __forceinline__ void compact_mag_item(const CompactArgs& a0, const MagOut& o,
                                                  uint32_t chunk, const MagState& st,
-                                                 float (&x)[kMQ], SH& sh, uint32_t par) {
+                                                 float (&x)[MagGeo<NW>::kQ], SH& sh, uint32_t par) {
   const int tid = threadIdx.x;
   const uint32_t base = chunk * (uint32_t)kChunk;
   const bool full = (uint64_t)base + kChunk <= a0.n;
@@ -799,7 +808,7 @@ __device__ __forceinline__ void compact_mag_item(const CompactArgs& a0, const Ma
   P.cand_all = P.t_hi >= 0x7f800001u;
   P.T_hi = __uint_as_float(P.cand_all ? 0x7f800000u : P.t_hi);
   if (fast) {
-    compact_mag_body<true>(o, P, x, sh, chunk, st.sbin, par);
+    compact_mag_body<true, SH, NW>(o, P, x, sh, chunk, st.sbin, par);
   } else if (none) {                                       // k = 0: nothing listed
     SH::barrier();
     if (tid == 0) {
@@ -807,23 +816,30 @@ __device__ __forceinline__ void compact_mag_item(const CompactArgs& a0, const Ma
       o.ccnt[chunk] = 0;
     }
   } else {                                                 // rare: exact integer predicate
-    mag_exact_bits(P, x, base + (uint32_t)((tid >> 6) * 256 + lane_id()));
-    compact_mag_body<false>(o, P, x, sh, chunk, st.sbin, par);
+    mag_exact_bits<NW>(P, x, base + (uint32_t)((tid >> 6) * 256 + lane_id()));
+    compact_mag_body<false, SH, NW>(o, P, x, sh, chunk, st.sbin, par);
   }
 }
 
 #ifndef FC_MAG1_WAVES_PER_EU
 #define FC_MAG1_WAVES_PER_EU 8
 #endif
-__global__ __launch_bounds__(kCBlock, FC_MAG1_WAVES_PER_EU) void k_compact_mag1(CompactArgs a0) {
+template <int NW>
+__device__ __forceinline__ void compact_mag_wg(const CompactArgs& a0) {
   __shared__ __attribute__((aligned(16))) MagShared sh;
   const uint32_t client = blockIdx.y, chunk = blockIdx.x;
-  float x[kMQ];
-  mag_load(mag_g(a0, client), chunk, a0.n, x);             // g first, state behind it
+  float x[MagGeo<NW>::kQ];
+  mag_load<NW>(mag_g(a0, client), chunk, a0.n, x);       // g first, state behind it
   const MagState st = mag_state(mag_S(a0, client));
   if (threadIdx.x == 0) sh.ncand[0] = 0;
-  compact_mag_item(a0, mag_out(a0, client), chunk, st, x, sh, 0u);
+  compact_mag_item<NW>(a0, mag_out(a0, client), chunk, st, x, sh, 0u);
 }
+// 512 threads (8 waves x 16 elements per lane)
+__global__ __launch_bounds__(kCBlock, FC_MAG1_WAVES_PER_EU) void k_compact_mag1(CompactArgs a0) {
+  compact_mag_wg<8>(a0);
+}
+// (A 256-thread form, 4 waves x 32 elements per lane, measured equal at 128 VGPRs and slower
+// with spills at 80-96: DESIGN.md §Lessons.)
 
 // --------------------------------------------------------------------------------------
 // k_resolve: exact T64 from the bracket's candidates (fast path, one launch).
