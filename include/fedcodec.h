@@ -54,6 +54,7 @@ typedef void* fc_stream_t; /* hipStream_t */
 #define FC_CODEC_RAND 2
 #define FC_CODEC_DROPOUT_BIASED 3
 #define FC_CODEC_DROPOUT_UNBIASED 4
+#define FC_CODEC_QSGD 5      /* opt-in: the reference raises NotImplementedError (:62-64)    */
 
 /* key sources for fc_topk_encode */
 #define FC_KEY_MAGNITUDE 0   /* |g| (top-k) */
@@ -62,6 +63,7 @@ typedef void* fc_stream_t; /* hipStream_t */
 /* packet formats */
 #define FC_FMT_IDXVAL 0      /* uint32 idx[] ascending + float val[] */
 #define FC_FMT_BITMAP 1      /* uint32 bitmap[ceil(N/8192)*256] + float val[] */
+#define FC_FMT_QSGD 2        /* packed W-bit codes (sign | level), fc_qsgd_code_words */
 
 /* Slotted packet layout: the gradient is cut into chunks of FC_CHUNK elements; chunk c's
  * entries (ascending index order) live at [c*FC_CHUNK, c*FC_CHUNK + cnt[c]) of idx/val (and
@@ -188,6 +190,26 @@ int fc_weighted_sum_dense(const float* const* rows, const float* w, int m, uint6
  * fc_weighted_sum_dense with weights 1.0) divided once by the row count: x = fl(x / d), in
  * place, x a DEVICE fp32[n] (16-B aligned). */
 int fc_div_scalar(float* x, uint64_t n, float d, fc_stream_t stream);
+
+/* ---- QSGD quantiser (compression.py:62-74, the reference's commented formula; opt-in,
+ * parity unpinned with respect to the reference, pinned to oracle/qsgd_oracle.py) ------
+ * q_i = sign(g_i) * ||g|| / (s tau) * floor(s |g_i| / ||g|| + U_i), s = 2^bits (1..14),
+ * tau = 1 + min(sqrt(n)/s, n/s^2), U_i from Philox(seed, offset).  Codes: W = 4/8/16-bit
+ * (sign | level) packed little-endian into code_words >= fc_qsgd_code_words(n, bits) uint32
+ * (16-B aligned).  The header records ||g|| (double, field p), bits (field k), the Philox
+ * key/counter, codec FC_CODEC_QSGD and format FC_FMT_QSGD.  ws: fc_qsgd_workspace_bytes(),
+ * zeroed once.  Decoders take fc_packet_view with idx = codes. */
+uint64_t fc_qsgd_code_words(uint64_t n, int bits);
+size_t fc_qsgd_workspace_bytes(void);
+int fc_qsgd_encode(const float* g, uint64_t n, int bits, uint64_t seed, uint64_t offset,
+                   uint32_t* codes, uint64_t code_words, fc_packet_hdr* hdr, void* ws,
+                   size_t ws_bytes, fc_stream_t stream);
+int fc_qsgd_decode(const fc_packet_view* pkt, uint64_t n, float* out, fc_stream_t stream);
+/* FedAVG over QSGD packets (views_dev: DEVICE array of m views, weights in the views):
+ * out = fl(... fl(+0 + fl(w_0 q_0)) ...) in row order (gar.py:44); continue_sum != 0 folds
+ * into the partial sum already in out. */
+int fc_qsgd_decode_accumulate(const fc_packet_view* views_dev, int m, uint64_t n, float* out,
+                              int continue_sum, fc_stream_t stream);
 
 /* ---- measurement: HIP events around selected kernels, on the stream they run on -------
  * mask: FC_TIME_* bits.  Between fc_timing_begin and fc_timing_end every launch of a

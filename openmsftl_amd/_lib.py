@@ -16,8 +16,9 @@ LIB_PATH = os.path.join(HERE, "libfedcodec.so")
 FC_OK = 0
 FC_STATUS_OK, FC_STATUS_RETRY_EXACT, FC_STATUS_OVERFLOW, FC_STATUS_TIMEOUT = 0, 1, 2, 3
 FC_CODEC_TOP, FC_CODEC_RAND, FC_CODEC_DROPOUT_BIASED, FC_CODEC_DROPOUT_UNBIASED = 1, 2, 3, 4
+FC_CODEC_QSGD = 5
 FC_KEY_MAGNITUDE, FC_KEY_PHILOX = 0, 1
-FC_FMT_IDXVAL, FC_FMT_BITMAP = 0, 1
+FC_FMT_IDXVAL, FC_FMT_BITMAP, FC_FMT_QSGD = 0, 1, 2
 FC_CHUNK = 8192
 HDR_BYTES = 96
 
@@ -84,6 +85,11 @@ SIGNATURES = {
     "fc_decode_accumulate_continue": (_i32, [_vp, _i32, _i32, _u64, _vp, _vp]),
     "fc_weighted_sum_dense": (_i32, [_vp, _vp, _i32, _u64, _vp, _vp]),
     "fc_div_scalar": (_i32, [_vp, _u64, ctypes.c_float, _vp]),
+    "fc_qsgd_code_words": (_u64, [_u64, _i32]),
+    "fc_qsgd_workspace_bytes": (_sz, []),
+    "fc_qsgd_encode": (_i32, [_vp, _u64, _i32, _u64, _u64, _vp, _u64, _vp, _vp, _sz, _vp]),
+    "fc_qsgd_decode": (_i32, [ctypes.POINTER(PacketView), _u64, _vp, _vp]),
+    "fc_qsgd_decode_accumulate": (_i32, [_vp, _i32, _u64, _vp, _i32, _vp]),
     "fc_timing_begin": (_i32, [ctypes.c_uint32]),
     "fc_timing_end": (_i32, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)]),
 }

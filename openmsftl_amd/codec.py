@@ -365,3 +365,86 @@ def div_scalar(x: torch.Tensor, d: float) -> torch.Tensor:
     L.check(lib.fc_div_scalar(_vp(x), x.numel(), ctypes.c_float(d), _stream(x.device)),
             "fc_div_scalar")
     return x
+
+
+# ---- QSGD (compression.py:62-74; opt-in, parity unpinned: oracle/qsgd_oracle.py) ----------
+@dataclass
+class QsgdPacket:
+    codes: torch.Tensor          # uint32[fc_qsgd_code_words(n, bits)]
+    hdr: torch.Tensor            # uint8[HDR_BYTES]
+    n: int
+    bits: int
+
+    @classmethod
+    def alloc(cls, n: int, bits: int, device) -> "QsgdPacket":
+        lib = L.load()
+        words = int(lib.fc_qsgd_code_words(n, bits))
+        if words == 0:
+            raise ValueError(f"bits={bits} outside [1, 14]")
+        return cls(torch.empty(words, dtype=torch.int32, device=device),
+                   torch.zeros(L.HDR_BYTES, dtype=torch.uint8, device=device), n, bits)
+
+    def view(self, weight: float = 1.0) -> L.PacketView:
+        v = L.PacketView()
+        v.idx = self.codes.data_ptr()
+        v.hdr = self.hdr.data_ptr()
+        v.weight = weight
+        return v
+
+    def header(self) -> L.PacketHdr:
+        return L.PacketHdr.from_buffer_copy(bytes(self.hdr.cpu().numpy()))
+
+
+_QSGD_WS = {}
+
+
+def encode_qsgd(g: torch.Tensor, bits: int, *, seed: int = 0, offset: int = 0,
+                packet: Optional[QsgdPacket] = None) -> QsgdPacket:
+    """QSGD codes of a device gradient (two streaming passes: ||g||, then quantise)."""
+    lib = L.load()
+    _require_cuda_f32(g)
+    n, dev = g.numel(), g.device
+    if packet is None:
+        packet = QsgdPacket.alloc(n, bits, dev)
+    key = (dev.index,)
+    ws = _QSGD_WS.get(key)
+    if ws is None:
+        ws = _QSGD_WS[key] = torch.zeros(int(lib.fc_qsgd_workspace_bytes()), dtype=torch.uint8,
+                                         device=dev)
+    L.check(lib.fc_qsgd_encode(_vp(g), n, bits, seed, offset, _vp(packet.codes),
+                               packet.codes.numel(), _vp(packet.hdr), _vp(ws), ws.numel(),
+                               _stream(dev)), "fc_qsgd_encode")
+    return packet
+
+
+def decode_qsgd(packet: QsgdPacket, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    lib = L.load()
+    dev = packet.codes.device
+    if out is None:
+        out = torch.empty(packet.n, dtype=torch.float32, device=dev)
+    _require_cuda_f32(out, "out")
+    v = packet.view()
+    L.check(lib.fc_qsgd_decode(ctypes.byref(v), packet.n, _vp(out), _stream(dev)), "fc_qsgd_decode")
+    return out
+
+
+def decode_accumulate_qsgd(packets: Sequence[QsgdPacket], weights, out: Optional[torch.Tensor] = None,
+                           continue_sum: bool = False) -> torch.Tensor:
+    """FedAVG over QSGD packets: gar.py:44 on the dense rows they decode to (bit-exact)."""
+    lib = L.load()
+    if not packets:
+        raise ValueError("no packets")
+    n, dev = packets[0].n, packets[0].codes.device
+    if any(p.n != n for p in packets):
+        raise ValueError("packets must share n")
+    if out is None:
+        if continue_sum:
+            raise ValueError("continue_sum needs the partial sum in `out`")
+        out = torch.empty(n, dtype=torch.float32, device=dev)
+    _require_cuda_f32(out, "out")
+    arr = (L.PacketView * len(packets))(*[p.view(float(w)) for p, w in zip(packets, weights)])
+    views = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(dev)
+    L.check(lib.fc_qsgd_decode_accumulate(_vp(views), len(packets), n, _vp(out),
+                                          int(continue_sum), _stream(dev)),
+            "fc_qsgd_decode_accumulate")
+    return out

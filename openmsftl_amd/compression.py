@@ -63,6 +63,10 @@ class Compression:
         self.rng = compression_config.get("rng", "numpy")
         self.seed = int(compression_config.get("seed", 0))
         self.device = compression_config.get("device", None)
+        # 'qsgd': the reference raises NotImplementedError (compression.py:62-64); "native"
+        # opts into this build's QSGD (the reference's commented formula, :65-74; num_bits as
+        # the reference reads it; Philox keyed by 'seed'; parity unpinned: DESIGN.md §6)
+        self.qsgd = compression_config.get("qsgd", None)
         self._calls = 0
 
     # ------------------------------------------------------------------------------------
@@ -72,6 +76,8 @@ class Compression:
         fn = self.compression_function
         if fn == 'full':
             return grad
+        if fn == 'qsgd' and self.qsgd == 'native':
+            return self._qsgd(grad)
         if fn not in ('top', 'rand', 'dropout-biased', 'dropout-unbiased'):
             raise NotImplementedError          # 'qsgd' (:62-64) and unknown names (:76-77)
         L.load()                               # the HIP path is mandatory
@@ -120,6 +126,17 @@ class Compression:
         return out if on_device else out.cpu().numpy()
 
     # ------------------------------------------------------------------------------------
+    def _qsgd(self, grad):
+        """compression.py:65-74 (opt-in): dense float32 result of the QSGD codec."""
+        L.load()
+        on_device = isinstance(grad, torch.Tensor)
+        g = self._to_device(grad)
+        if g.numel() == 0:
+            return grad.clone() if on_device else np.zeros_like(grad)
+        pkt = codec.encode_qsgd(g, int(self.num_bits), seed=self.seed, offset=self._next_offset())
+        out = codec.decode_qsgd(pkt)
+        return out if on_device else out.cpu().numpy()
+
     def _next_offset(self) -> int:
         self._calls += 1
         return self._calls

@@ -466,6 +466,78 @@ int fc_decode_accumulate_continue(const fc_packet_view* views_dev, int m, int fo
   return decode_accumulate(views_dev, m, format, n, acc, true, stream);
 }
 
+uint64_t fc_qsgd_code_words(uint64_t n, int bits) {
+  if (bits < 1 || bits > 14) return 0;
+  return (n + kQsgdElems - 1) / kQsgdElems * (uint64_t)(qsgd_width(bits) * kQsgdElems / 32);
+}
+size_t fc_qsgd_workspace_bytes(void) { return 64 + 8 * (size_t)kQsgdNormGrid; }
+
+static uint32_t stream_grid(uint64_t items) {
+  uint64_t b = (items + kBlock - 1) / kBlock;
+  if (b < 1) b = 1;
+  if (b > 4096) b = 4096;
+  return (uint32_t)b;
+}
+
+int fc_qsgd_encode(const float* g, uint64_t n, int bits, uint64_t seed, uint64_t offset,
+                   uint32_t* codes, uint64_t code_words, fc_packet_hdr* hdr, void* ws,
+                   size_t ws_bytes, fc_stream_t stream) {
+  FC_CHECK(g && codes && hdr && ws, "NULL argument");
+  FC_CHECK(n >= 1 && n <= 0xffffffffull, "n=%llu outside [1, 2^32-1]", (unsigned long long)n);
+  FC_CHECK(bits >= 1 && bits <= 14, "bits=%d outside [1, 14]", bits);
+  FC_CHECK(((uintptr_t)g & 15) == 0 && ((uintptr_t)codes & 15) == 0, "g and codes must be 16-byte aligned");
+  FC_CHECK(code_words >= fc_qsgd_code_words(n, bits), "code_words %llu < %llu needed",
+           (unsigned long long)code_words, (unsigned long long)fc_qsgd_code_words(n, bits));
+  if (ws_bytes < fc_qsgd_workspace_bytes())
+    return fail(FC_ERR_WORKSPACE, "workspace %zu B < %zu B needed", ws_bytes, fc_qsgd_workspace_bytes());
+  hipStream_t s = (hipStream_t)stream;
+  char* w = static_cast<char*>(ws);
+  uint64_t ng = (n / 4 + kBlock - 1) / kBlock;                 // fixed for a given n
+  if (ng < 1) ng = 1;
+  if (ng > (uint64_t)kQsgdNormGrid) ng = kQsgdNormGrid;
+  {
+    TimedLaunch t(FC_TIME_SAMPLE, s);
+    hipLaunchKernelGGL(k_qsgd_norm, dim3((uint32_t)ng), dim3(kBlock), 0, s, g, n, bits, seed, offset,
+                       reinterpret_cast<double*>(w + 64), reinterpret_cast<uint32_t*>(w), hdr);
+    FC_LAUNCHED("k_qsgd_norm");
+  }
+  TimedLaunch t(FC_TIME_COMPACT, s);
+  hipLaunchKernelGGL(k_qsgd_quant, dim3(stream_grid((n + kQsgdElems - 1) / kQsgdElems)), dim3(kBlock), 0, s,
+                     g, n, bits, seed, offset, hdr, codes);
+  FC_LAUNCHED("k_qsgd_quant");
+  return FC_OK;
+}
+
+int fc_qsgd_decode(const fc_packet_view* pkt, uint64_t n, float* out, fc_stream_t stream) {
+  FC_CHECK(pkt && out && pkt->idx && pkt->hdr, "NULL argument");
+  FC_CHECK(n >= 1 && n <= 0xffffffffull, "bad n");
+  FC_CHECK(((uintptr_t)out & 15) == 0 && ((uintptr_t)pkt->idx & 15) == 0, "out and codes must be 16-byte aligned");
+  QsgdDecodeArgs a;
+  memset(&a, 0, sizeof a);
+  a.one = *pkt; a.m = 1; a.n = n; a.out = out;
+  hipStream_t s = (hipStream_t)stream;
+  TimedLaunch t(FC_TIME_DECODE, s);
+  hipLaunchKernelGGL(k_qsgd_decode<false>, dim3(stream_grid((n + kQsgdElems - 1) / kQsgdElems)), dim3(kBlock), 0, s, a);
+  FC_LAUNCHED("k_qsgd_decode");
+  return FC_OK;
+}
+
+int fc_qsgd_decode_accumulate(const fc_packet_view* views_dev, int m, uint64_t n, float* out,
+                              int continue_sum, fc_stream_t stream) {
+  FC_CHECK(views_dev && out, "NULL argument");
+  FC_CHECK(m >= 1, "m=%d < 1", m);
+  FC_CHECK(n >= 1 && n <= 0xffffffffull, "bad n");
+  FC_CHECK(((uintptr_t)out & 15) == 0, "out must be 16-byte aligned");
+  QsgdDecodeArgs a;
+  memset(&a, 0, sizeof a);
+  a.views = views_dev; a.m = m; a.acc_in = continue_sum != 0; a.n = n; a.out = out;
+  hipStream_t s = (hipStream_t)stream;
+  TimedLaunch t(FC_TIME_DECODE, s);
+  hipLaunchKernelGGL(k_qsgd_decode<true>, dim3(stream_grid((n + kQsgdElems - 1) / kQsgdElems)), dim3(kBlock), 0, s, a);
+  FC_LAUNCHED("k_qsgd_decode(acc)");
+  return FC_OK;
+}
+
 int fc_div_scalar(float* x, uint64_t n, float d, fc_stream_t stream) {
   FC_CHECK(x != nullptr, "x is NULL");
   FC_CHECK(n >= 1, "n=0");

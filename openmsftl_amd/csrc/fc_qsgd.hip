@@ -1,0 +1,214 @@
+// fc_qsgd.hip — QSGD stochastic quantiser (the 'qsgd' codec of compression.py:62-74) for
+// MI355X (gfx950).  SURVEY.md §8(f) row 2: the reference raises NotImplementedError and keeps
+// the formula only as a comment, so this codec is opt-in and "parity unpinned" with respect to
+// the reference; it is pinned to oracle/qsgd_oracle.py, which restates the comment:
+//
+//   s = 2^num_bits,  tau = 1 + min(sqrt(d)/s, d/s^2),  norm = ||g||_2
+//   q_i = sign(g_i) * norm / (s * tau) * floor(s * |g_i| / norm + U_i),  U_i ~ U[0, 1)
+//
+// (Alistarh et al., "QSGD", NeurIPS 2017; the reference's comment divides by tau, so
+// E[q] = g / tau.)  Exact arithmetic of this build, shared with the oracle:
+//   norm  = sqrt(sum of g_i^2 in fp64), the sum in a fixed order (k_qsgd_norm), stored as a
+//           double in the header's `p` field;
+//   U_i   = (philox_word(i) >> 8) * 2^-24;
+//   l_i   = floor(fl64(fl64(s * |g_i|) / norm) + U_i)   in [0, s]; 0 when not finite;
+//   code  = signbit(g_i) << (W - 1) | l_i,  W = 4 (bits <= 2), 8 (<= 6), 16 (<= 14) bits,
+//           packed little-endian, 32 / W codes per uint32;
+//   value = (float)(+-(norm / (s * tau)) * l_i)   (fp64 product, one rounding to fp32).
+// Bytes: encode 8N (norm pass + quantise pass) + N W / 8; decode N W / 8 + 4N.
+#include "fc_state.h"
+
+namespace fc {
+
+constexpr int kQsgdNormGrid = 1024;            // fixed: the fp64 sum order depends on it
+constexpr int kQsgdElems = 8;                  // elements per thread per step (quant/decode)
+
+__host__ __device__ inline int qsgd_width(int bits) { return bits <= 2 ? 4 : bits <= 6 ? 8 : 16; }
+
+struct QsgdParams {                            // from the header (decode) or the encode args
+  double norm, scale;                          // scale = norm / (s * tau)
+  double s;
+  int width;
+};
+
+__device__ __forceinline__ double qsgd_tau(double d, double s) {
+  const double a = sqrt(d) / s, b = d / (s * s);
+  return 1.0 + (a < b ? a : b);
+}
+
+// ---- pass 1: ||g||_2 (fp64, fixed order), header -------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_qsgd_norm(const float* __restrict__ g, uint64_t n,
+                                                      int bits, uint64_t seed, uint64_t offset,
+                                                      double* partial, uint32_t* ticket,
+                                                      fc_packet_hdr* hdr) {
+  __shared__ double s_red[kBlock / 64];
+  __shared__ uint32_t s_flag;
+  const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  double acc = 0.0;
+  const uint64_t n4 = n / 4;
+  for (uint64_t q = (uint64_t)blockIdx.x * kBlock + tid; q < n4; q += (uint64_t)gridDim.x * kBlock) {
+    const float4 v = load4_full(g + 4 * q);
+    acc += (double)v.x * v.x; acc += (double)v.y * v.y;
+    acc += (double)v.z * v.z; acc += (double)v.w * v.w;
+  }
+  if (blockIdx.x == 0 && tid < (int)(n - 4 * n4)) {            // tail (< 4 elements)
+    const double t = g[4 * n4 + tid];
+    acc += t * t;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if (lane == 0) s_red[w] = acc;
+  __syncthreads();
+  if (tid == 0) {
+    double b = 0.0;
+    for (int i = 0; i < kBlock / 64; ++i) b += s_red[i];
+    st_agent(reinterpret_cast<uint64_t*>(&partial[blockIdx.x]), (uint64_t)__double_as_longlong(b));
+  }
+  if (!last_block_arrive_sc1(ticket, gridDim.x, &s_flag)) return;
+  // ---- last workgroup: fixed-order sum of the partials, header --------------------------
+  double t = 0.0;
+  for (uint32_t i = (uint32_t)tid; i < gridDim.x; i += kBlock)
+    t += __longlong_as_double((long long)ld_agent(reinterpret_cast<const uint64_t*>(&partial[i])));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+  __syncthreads();
+  if (lane == 0) s_red[w] = t;
+  __syncthreads();
+  if (tid == 0) {
+    double sum = 0.0;
+    for (int i = 0; i < kBlock / 64; ++i) sum += s_red[i];
+    hdr->thresh = 0; hdr->lower = 0;
+    hdr->n = (uint32_t)n; hdr->k = (uint32_t)bits; hdr->n_entries = (uint32_t)n;
+    hdr->index_bits = 0; hdr->codec = FC_CODEC_QSGD; hdr->status = FC_STATUS_OK;
+    hdr->n_definite = 0; hdr->n_cand = 0;
+    hdr->seed = seed; hdr->offset = offset; hdr->p = sqrt(sum);
+    hdr->chunk = 0; hdr->format = FC_FMT_QSGD; hdr->key_mode = FC_KEY_PHILOX;
+    hdr->reserved[0] = hdr->reserved[1] = hdr->reserved[2] = 0;
+    *ticket = 0;                                                  // for the next encode
+  }
+}
+
+__device__ __forceinline__ QsgdParams qsgd_params(double norm, int bits, uint64_t n) {
+  QsgdParams q;
+  q.norm = norm;
+  q.s = (double)(1u << bits);
+  q.scale = norm / (q.s * qsgd_tau((double)n, q.s));
+  q.width = qsgd_width(bits);
+  return q;
+}
+
+__device__ __forceinline__ uint32_t qsgd_code(float x, uint32_t word, const QsgdParams& q) {
+  const double u = (double)(word >> 8) * (1.0 / 16777216.0);
+  const double r = (q.s * (double)__builtin_fabsf(x)) / q.norm;
+  const double f = floor(r + u);
+  const uint32_t l = (f >= 0.0 && f <= q.s) ? (uint32_t)f : 0u;   // NaN / inf -> 0
+  return ((__float_as_uint(x) >> 31) << (q.width - 1)) | l;
+}
+__device__ __forceinline__ float qsgd_value(uint32_t code, const QsgdParams& q) {
+  const uint32_t l = code & ((1u << (q.width - 1)) - 1u);
+  const double v = q.scale * (double)l;
+  return (float)(((code >> (q.width - 1)) & 1u) ? -v : v);
+}
+
+// ---- pass 2: quantise; thread = 8 consecutive elements -> 8 codes ----------------------------
+__global__ __launch_bounds__(kBlock) void k_qsgd_quant(const float* __restrict__ g, uint64_t n,
+                                                       int bits, uint64_t seed, uint64_t offset,
+                                                       const fc_packet_hdr* hdr, uint32_t* codes) {
+  const QsgdParams q = qsgd_params(hdr->p, bits, n);
+  const uint64_t groups = (n + kQsgdElems - 1) / kQsgdElems;
+  for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < groups;
+       t += (uint64_t)gridDim.x * kBlock) {
+    const uint64_t e = t * kQsgdElems;
+    float x[8];
+    if (e + 8 <= n) {
+      const float4 a = load4_full(g + e), b = load4_full(g + e + 4);
+      x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = e + j < n ? g[e + j] : 0.f;
+    }
+    const uint4 r0 = philox_block(e >> 2, seed, offset), r1 = philox_block((e >> 2) + 1, seed, offset);
+    const uint32_t wd[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+    uint32_t c[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) c[j] = e + j < n ? qsgd_code(x[j], wd[j], q) : 0u;
+    if (q.width == 4) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v |= c[j] << (4 * j);
+      codes[t] = v;
+    } else if (q.width == 8) {
+      reinterpret_cast<uint2*>(codes)[t] = make_uint2(c[0] | c[1] << 8 | c[2] << 16 | c[3] << 24,
+                                                      c[4] | c[5] << 8 | c[6] << 16 | c[7] << 24);
+    } else {
+      reinterpret_cast<uint4*>(codes)[t] = make_uint4(c[0] | c[1] << 16, c[2] | c[3] << 16,
+                                                      c[4] | c[5] << 16, c[6] | c[7] << 16);
+    }
+  }
+}
+
+// ---- decode (ACC: FedAVG over packets in row order, from +0 as np.sum) ----------------------
+struct QsgdDecodeArgs {
+  const fc_packet_view* views;   // ACC
+  fc_packet_view one;            // !ACC
+  int m, acc_in;
+  uint64_t n;
+  float* out;
+};
+
+__device__ __forceinline__ void qsgd_unpack(const uint32_t* codes, uint64_t t, int width,
+                                            uint32_t (&c)[8]) {
+  typedef __attribute__((address_space(1))) const uint32_t gu;
+  if (width == 4) {
+    const uint32_t v = ((gu*)codes)[t];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) c[j] = (v >> (4 * j)) & 0xfu;
+  } else if (width == 8) {
+    typedef __attribute__((address_space(1))) const fc_u32x2 gu2;
+    const fc_u32x2 v = ((gu2*)codes)[t];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { c[j] = (v.x >> (8 * j)) & 0xffu; c[4 + j] = (v.y >> (8 * j)) & 0xffu; }
+  } else {
+    typedef __attribute__((address_space(1))) const fc_u32x4 gu4;
+    const fc_u32x4 v = ((gu4*)codes)[t];
+    c[0] = v.x & 0xffffu; c[1] = v.x >> 16; c[2] = v.y & 0xffffu; c[3] = v.y >> 16;
+    c[4] = v.z & 0xffffu; c[5] = v.z >> 16; c[6] = v.w & 0xffffu; c[7] = v.w >> 16;
+  }
+}
+
+template <bool ACC>
+__global__ __launch_bounds__(kBlock) void k_qsgd_decode(QsgdDecodeArgs a) {
+  const uint64_t n = a.n, groups = (n + kQsgdElems - 1) / kQsgdElems;
+  const int M = ACC ? a.m : 1;
+  for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < groups;
+       t += (uint64_t)gridDim.x * kBlock) {
+    const uint64_t e = t * kQsgdElems;
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = (ACC && a.acc_in && e + j < n) ? a.out[e + j] : 0.f;
+    for (int m = 0; m < M; ++m) {                                // rows in order (gar.py:44)
+      const fc_packet_view& v = ACC ? a.views[m] : a.one;
+      const fc_packet_hdr* h = v.hdr;
+      const QsgdParams q = qsgd_params(h->p, (int)h->k, n);
+      uint32_t c[8];
+      qsgd_unpack(v.idx, t, q.width, c);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = qsgd_value(c[j], q);
+        acc[j] = ACC ? __fadd_rn(acc[j], __fmul_rn(d, v.weight)) : d;
+      }
+    }
+    if (e + 8 <= n) {
+      *reinterpret_cast<float4*>(a.out + e) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+      *reinterpret_cast<float4*>(a.out + e + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) if (e + j < n) a.out[e + j] = acc[j];
+    }
+  }
+}
+
+template __global__ void k_qsgd_decode<true>(QsgdDecodeArgs);
+template __global__ void k_qsgd_decode<false>(QsgdDecodeArgs);
+
+}  // namespace fc

@@ -2,4 +2,5 @@
 //   hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fPIC -shared fedcodec.hip
 #include "fc_topk.hip"
 #include "fc_decode.hip"
+#include "fc_qsgd.hip"
 #include "fc_capi.hip"

@@ -530,3 +530,71 @@ def test_aggregator_top_packets_match_dense_reference(sizes):
     assert agg.agg_grad.tobytes() == ref.tobytes()
     with pytest.raises(Exception, match="Client List is Empty"):
         agg.aggregate_grads([])
+
+
+# ---- QSGD (opt-in; parity unpinned w.r.t. the reference: pinned to oracle/qsgd_oracle.py) --
+QSGD_CASES = [(1, 1), (5, 2), (4097, 2), (100_003, 1), (100_003, 4), (65_536, 8), (70_001, 14),
+              ((1 << 20) + 3, 2)]
+
+
+@pytest.mark.parametrize("n,bits", QSGD_CASES)
+def test_qsgd_codes_and_values_match_oracle(n, bits):
+    from oracle import qsgd_oracle as qo
+    codec = _codec()
+    rng = np.random.default_rng(n + bits)
+    g = (rng.standard_normal(n) * 10.0 ** rng.uniform(-4, 1)).astype(np.float32)
+    if n > 10:
+        g[:3] = [0.0, -0.0, 1e-40]
+    seed, off = 1234 + bits, 7
+    pkt = codec.encode_qsgd(torch.from_numpy(g).cuda(), bits, seed=seed, offset=off)
+    h = pkt.header()
+    assert h.codec == 5 and h.format == 2 and h.k == bits and h.status == 0
+    assert h.p == pytest.approx(qo.norm64(g), rel=1e-12)        # fp64, reassociated sum
+    words = pkt.codes.cpu().numpy().view(np.uint32)
+    want = qo.encode(g, bits, seed, off, h.p)
+    assert words[: want.shape[0]].tobytes() == want.tobytes()
+    out = codec.decode_qsgd(pkt).cpu().numpy()
+    assert out.tobytes() == qo.decode(want, n, bits, h.p).tobytes()
+
+
+def test_qsgd_fedavg_and_statistics():
+    """FedAVG over QSGD packets == the +0-started row-order sum of the decoded rows; and the
+    quantiser's expectation is g / tau (the reference comment's scaling)."""
+    from oracle import qsgd_oracle as qo
+    codec = _codec()
+    M, n, bits = 9, 50_021, 2
+    rng = np.random.default_rng(11)
+    grads = [rng.standard_normal(n).astype(np.float32) for _ in range(M)]
+    pkts = [codec.encode_qsgd(torch.from_numpy(x).cuda(), bits, seed=i, offset=1)
+            for i, x in enumerate(grads)]
+    w = rng.uniform(0.01, 1, M).astype(np.float32)
+    agg = codec.decode_accumulate_qsgd(pkts, list(w)).cpu().numpy()
+    rows = [qo.decode(p.codes.cpu().numpy().view(np.uint32), n, bits, p.header().p) for p in pkts]
+    assert agg.tobytes() == go.sequential_weighted_sum(rows, w).tobytes()
+    # unbiased up to 1/tau: mean over 200 seeds of one gradient
+    x = grads[0][:4096].copy()
+    gx = torch.from_numpy(x).cuda()
+    acc = np.zeros(4096, np.float64)
+    for s in range(200):
+        acc += codec.decode_qsgd(codec.encode_qsgd(gx, 4, seed=s)).cpu().numpy()
+    s4 = 16.0
+    t = qo.tau(4096, s4)
+    err = np.abs(acc / 200 - x / t)
+    bound = 4 * qo.norm64(x) / (s4 * t) / np.sqrt(200)           # ~4 sigma of one level step
+    assert (err < bound).mean() > 0.999
+
+
+def test_qsgd_compression_surface():
+    """'qsgd' raises NotImplementedError as in the reference unless opted in."""
+    from openmsftl_amd import Compression
+    from oracle import qsgd_oracle as qo
+    g = np.random.default_rng(2).standard_normal(10_007).astype(np.float32)
+    with pytest.raises(NotImplementedError):
+        Compression({"compression_function": "qsgd"}).compress(g)
+    C = Compression({"compression_function": "qsgd", "qsgd": "native", "num_bits": 2, "seed": 5})
+    out = C.compress(g)
+    assert out.dtype == np.float32 and out.shape == g.shape
+    levels = np.unique(np.abs(out))
+    assert levels.shape[0] <= 5                                   # 0..s levels, s = 4
+    want = qo.compress(g, 2, 5, 1, qo.norm64(g))
+    np.testing.assert_allclose(out, want, rtol=1e-6, atol=0)      # norm: fp64 reassociation

@@ -188,3 +188,24 @@ def test_hierarchical_merge_matches_reference(name):
     assert H.tobytes() == A.arr(name, "merged").tobytes()
     out = go.FedAvgOracle({}).aggregate(H)
     assert out.tobytes() == A.arr(name, "output").tobytes()
+
+
+def test_qsgd_oracle_packing_and_scaling():
+    """oracle/qsgd_oracle.py (parity unpinned w.r.t. the reference, which raises): the W-bit
+    packing round-trips, levels stay in [0, s], and values are +-norm/(s tau) * level."""
+    from oracle import qsgd_oracle as qo
+    rng = np.random.default_rng(3)
+    for n, bits in ((1, 1), (13, 2), (1000, 3), (4099, 8), (777, 14)):
+        g = rng.standard_normal(n).astype(np.float32)
+        nrm = qo.norm64(g)
+        words = qo.encode(g, bits, 9, 2, nrm)
+        W = qo.width(bits)
+        assert words.shape[0] == (n + 7) // 8 * (8 * W // 32)
+        lev, sign = qo.levels_and_signs(g, bits, 9, 2, nrm)
+        c = qo.unpack(words, n, bits)
+        assert np.array_equal(c, (sign << np.uint32(W - 1)) | lev)
+        assert lev.max() <= 2 ** bits
+        v = qo.decode(words, n, bits, nrm)
+        s = 2.0 ** bits
+        np.testing.assert_array_equal(np.abs(v), (nrm / (s * qo.tau(n, s)) * lev).astype(np.float32))
+        assert np.array_equal(np.signbit(v) & (lev > 0), np.signbit(g) & (lev > 0))
