@@ -199,6 +199,7 @@ def main():
                                "frac": round(step_gbps / world / HBM_PEAK_GBPS, 4)}}
     if rank == 0 and not args.no_single:
         extra["single_gradient"] = single_gradient(torch, codec, grads[0], k, n)
+        extra["qsgd_single_gradient"] = qsgd_single(torch, codec, grads[0], n)
 
     cpu = None
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
@@ -245,6 +246,27 @@ def single_gradient(torch, codec, g, k, n, iters=20):
             "grad_GBps": round(4.0 * n / dt / 1e9, 1),
             "alg_GBps": round(alg / dt / 1e9, 1),
             "hbm_frac": round(alg / dt / 1e9 / HBM_PEAK_GBPS, 4)}
+
+
+def qsgd_single(torch, codec, g, n, bits=2, iters=20):
+    """The opt-in QSGD codec (compression.py:62-74) on one 128 M gradient: encode (norm pass +
+    quantise pass, 8N read + N W/8 written) then dense decode (N W/8 read + 4N written)."""
+    pkt = codec.encode_qsgd(g, bits)
+    out = torch.empty_like(g)
+    for _ in range(3):
+        codec.encode_qsgd(g, bits, packet=pkt)
+        codec.decode_qsgd(pkt, out=out)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        codec.encode_qsgd(g, bits, packet=pkt)
+        codec.decode_qsgd(pkt, out=out)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / iters
+    wbytes = 4.0 if bits <= 2 else 8.0 if bits <= 6 else 16.0
+    alg = 8.0 * n + n * wbytes / 8.0 + n * wbytes / 8.0 + 4.0 * n
+    return {"n": n, "bits": bits, "us_per_encode_decode": round(dt * 1e6, 1),
+            "alg_GBps": round(alg / dt / 1e9, 1), "hbm_frac": round(alg / dt / 1e9 / HBM_PEAK_GBPS, 4)}
 
 
 if __name__ == "__main__":
