@@ -72,6 +72,9 @@ static uint32_t decode_grid(uint64_t n, uint32_t per_cu = kDecBlocksPerCU) {
   return g < nch ? g : nch;
 }
 
+#ifndef FC_MAX_SAMPLE_SEGS
+#define FC_MAX_SAMPLE_SEGS 1024
+#endif
 static SamplePlan make_plan(uint64_t n, uint64_t k) {
   SamplePlan P;
   memset(&P, 0, sizeof P);
@@ -83,7 +86,7 @@ static SamplePlan make_plan(uint64_t n, uint64_t k) {
   } else {
     uint64_t seg = n / 32 / 1024;
     if (seg < 64) seg = 64;
-    if (seg > 1024) seg = 1024;
+    if (seg > FC_MAX_SAMPLE_SEGS) seg = FC_MAX_SAMPLE_SEGS;
     P.nseg = (uint32_t)seg;
     const double S = (double)seg * 1024.0;
     const double q = (double)k / (double)n;
