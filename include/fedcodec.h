@@ -11,6 +11,8 @@
  *   Aggregator.aggregate_grads G build   aggregation.py:61-63   -> fc_decode_accumulate
  *   GAR.weighted_average / FedAvg        gar.py:32-46, 53-56    -> fc_decode_accumulate /
  *                                                                  fc_weighted_sum_dense
+ *   flatten_params / client delta        model_helper.py:11-35,
+ *                                        client.py:44,52-53     -> fc_flat_stage
  *   Aggregator.__merge_gradient          aggregation.py:80-93   -> fc_decode_accumulate /
  *                                                                  fc_weighted_sum_dense (w=1)
  *                                                                  + fc_div_scalar
@@ -184,6 +186,16 @@ int fc_decode_accumulate_continue(const fc_packet_view* views_dev, int m, int fo
  * pointers, w = DEVICE fp32[m]. */
 int fc_weighted_sum_dense(const float* const* rows, const float* w, int m, uint64_t n,
                           float* out, fc_stream_t stream);
+
+/* ---- flat-layout staging on the device (model_helper.py:11-35, client.py:44,52-53) ------
+ * params_dev: DEVICE array of `count` fp32 parameter pointers; offsets_dev: DEVICE
+ * uint64[count + 1] prefix offsets into the flat vector (max_size = largest parameter).
+ * scatter = 0: flat[off_p + i] <- param_p[i]; with grad != NULL first
+ *   grad = fl32(flat_old - param)  (client.py:53: current_weights - updated_model_weights),
+ *   i.e. flatten_params + the client delta in one pass, flat keeping the new weights;
+ * scatter = 1: param_p[i] <- flat[off_p + i]  (dist_weights_to_model / dist_grads_to_model). */
+int fc_flat_stage(const float* const* params_dev, const uint64_t* offsets_dev, int count,
+                  uint64_t max_size, float* flat, float* grad, int scatter, fc_stream_t stream);
 
 /* ---- hierarchical merge (aggregation.py:80-93): a cluster's mean
  * np.mean(G[s:e, :], axis=0) is the +0-started row-order sum (fc_decode_accumulate /

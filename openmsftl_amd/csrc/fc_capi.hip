@@ -541,6 +541,20 @@ int fc_qsgd_decode_accumulate(const fc_packet_view* views_dev, int m, uint64_t n
   return FC_OK;
 }
 
+int fc_flat_stage(const float* const* params_dev, const uint64_t* offsets_dev, int count,
+                  uint64_t max_size, float* flat, float* grad, int scatter, fc_stream_t stream) {
+  FC_CHECK(params_dev && offsets_dev && flat, "NULL argument");
+  FC_CHECK(count >= 1 && count <= 65535, "count=%d outside [1, 65535]", count);
+  FC_CHECK(!(scatter && grad), "scatter takes no grad");
+  uint64_t bx = (max_size + kBlock - 1) / kBlock;
+  if (bx < 1) bx = 1;
+  if (bx > 1024) bx = 1024;
+  hipLaunchKernelGGL(k_flat_stage, dim3((uint32_t)bx, (uint32_t)count), dim3(kBlock), 0,
+                     (hipStream_t)stream, params_dev, offsets_dev, flat, grad, scatter);
+  FC_LAUNCHED("k_flat_stage");
+  return FC_OK;
+}
+
 int fc_div_scalar(float* x, uint64_t n, float d, fc_stream_t stream) {
   FC_CHECK(x != nullptr, "x is NULL");
   FC_CHECK(n >= 1, "n=0");

@@ -649,6 +649,27 @@ __global__ __launch_bounds__(kBlock) void k_div_scalar(float* x, uint64_t n, flo
   }
 }
 
+// Flat-layout staging (model_helper.py:11-13 flatten_params; client.py:52-53
+// grad = current_weights - flatten_params): parameter p (grid.y) of `count` tensors is copied
+// to flat[off_p, off_p + size_p) and, when `grad` is set, grad = fl32(flat_old - flat_new)
+// (np.float32 subtraction) with flat updated in place to the new weights.  scatter = 1 runs
+// the inverse (dist_weights_to_model / dist_grads_to_model, model_helper.py:16-35).
+__global__ __launch_bounds__(kBlock) void k_flat_stage(const float* const* params, const uint64_t* offs,
+                                                       float* flat, float* grad, int scatter) {
+  const uint32_t p = blockIdx.y;
+  const uint64_t off = offs[p], size = offs[p + 1] - off;
+  float* prm = const_cast<float*>(params[p]);
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < size; i += (uint64_t)gridDim.x * kBlock) {
+    if (scatter) {
+      prm[i] = flat[off + i];
+    } else {
+      const float nw = prm[i];
+      if (grad) grad[off + i] = __fsub_rn(flat[off + i], nw);
+      flat[off + i] = nw;
+    }
+  }
+}
+
 template __global__ void k_decode<FC_FMT_IDXVAL, false, false>(DecodeArgs);
 template __global__ void k_decode<FC_FMT_IDXVAL, false, true>(DecodeArgs);
 template __global__ void k_decode<FC_FMT_BITMAP, false, false>(DecodeArgs);

@@ -598,3 +598,46 @@ def test_qsgd_compression_surface():
     assert levels.shape[0] <= 5                                   # 0..s levels, s = 4
     want = qo.compress(g, 2, 5, 1, qo.norm64(g))
     np.testing.assert_allclose(out, want, rtol=1e-6, atol=0)      # norm: fp64 reassociation
+
+
+# ---- flat-layout staging (model_helper.py:11-35, client.py:44,52-54) ---------------------------
+LENET_SHAPES = [(20, 1, 5, 5), (20,), (50, 20, 5, 5), (50,), (500, 800), (500,), (10, 500), (10,)]
+
+
+@pytest.mark.parametrize("shapes", [LENET_SHAPES, [(1,)], [(3,)] * 700 + [(70_001,)],
+                                    [(4_194_305,), (7,), (2, 3, 4)]])
+def test_flat_stage_matches_model_helper(shapes):
+    from openmsftl_amd.model_helper import FlatLayout
+    from oracle import model_helper_oracle as mo
+    rng = np.random.default_rng(len(shapes))
+    old = [rng.standard_normal(s).astype(np.float32) for s in shapes]
+    new = [(o - np.float32(0.01) * rng.standard_normal(s).astype(np.float32)).astype(np.float32)
+           for o, s in zip(old, shapes)]
+    if new[0].size > 2:                                    # exact-zero deltas and specials
+        new[0].flat[0] = old[0].flat[0]
+        old[0].flat[1], new[0].flat[1] = np.float32(-0.0), np.float32(0.0)
+        new[0].flat[2] = np.inf
+    params = [torch.from_numpy(o.copy()).cuda() for o in old]
+    lay = FlatLayout(params)
+    flat = lay.flatten()
+    cur = mo.flatten_params(old)
+    assert flat.cpu().numpy().tobytes() == cur.tobytes()
+    for p, x in zip(params, new):                           # "train": overwrite in place
+        p.copy_(torch.from_numpy(x))
+    grad = lay.client_delta(flat)
+    want_grad, want_cur = mo.client_step_delta(cur, new)
+    assert grad.cpu().numpy().tobytes() == want_grad.tobytes()
+    assert flat.cpu().numpy().tobytes() == want_cur.tobytes()
+    agg = torch.from_numpy(rng.standard_normal(lay.n).astype(np.float32)).cuda()
+    lay.scatter(agg)
+    back = mo.dist_weights_to_model(agg.cpu().numpy(), shapes)
+    for p, b in zip(params, back):
+        assert p.cpu().numpy().tobytes() == b.tobytes()
+
+
+def test_flat_stage_arguments():
+    from openmsftl_amd.model_helper import FlatLayout
+    with pytest.raises(TypeError):
+        FlatLayout([torch.zeros(3, dtype=torch.float64, device="cuda")])
+    with pytest.raises(ValueError):
+        FlatLayout([])

@@ -78,3 +78,13 @@ def test_argument_errors_do_not_touch_gpu(lib):
     assert rc == -1 and b"bad codec" in lib.fc_last_error()
     with pytest.raises(_lib.FedCodecError):
         _lib.check(lib.fc_decode_accumulate(None, 1, 0, 10, None, None), "decode_accumulate")
+
+
+def test_flat_stage_argument_errors(lib):
+    buf = ctypes.create_string_buffer(64)
+    addr = (ctypes.addressof(buf) + 15) & ~15
+    assert lib.fc_flat_stage(None, addr, 1, 1, addr, None, 0, None) == -1
+    assert lib.fc_flat_stage(addr, addr, 0, 1, addr, None, 0, None) == -1
+    assert b"count" in lib.fc_last_error()
+    assert lib.fc_flat_stage(addr, addr, 1, 1, addr, addr, 1, None) == -1
+    assert b"scatter" in lib.fc_last_error()
