@@ -444,11 +444,13 @@ static int decode_accumulate(const fc_packet_view* views_dev, int m, int format,
   FC_CHECK(((uintptr_t)acc & 15) == 0, "acc must be 16-byte aligned");
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid(decode_grid(n)), blk(kDBlock);
-  // <= kDecMaxM packets per launch; later launches continue the same left-to-right sum
-  for (int m0 = 0; m0 < m; m0 += kDecMaxM) {
+  // <= kSparseMaxM (idx/val) or kDecMaxM (bitmap) packets per launch; later launches
+  // continue the same left-to-right sum
+  const int per_launch = format == FC_FMT_IDXVAL ? kSparseMaxM : kDecMaxM;
+  for (int m0 = 0; m0 < m; m0 += per_launch) {
     DecodeArgs a;
     memset(&a, 0, sizeof a);
-    a.views = views_dev + m0; a.m = std::min(m - m0, kDecMaxM); a.acc_in = cont || m0 > 0;
+    a.views = views_dev + m0; a.m = std::min(m - m0, per_launch); a.acc_in = cont || m0 > 0;
     a.n = n; a.out = acc;
     TimedLaunch t(FC_TIME_DECODE, s);
     if (format == FC_FMT_IDXVAL)

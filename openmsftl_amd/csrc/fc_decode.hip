@@ -90,6 +90,14 @@ constexpr int kDecR = 4;                       // slot entries per thread per it
 #endif
 constexpr int kDecGroup = FC_DEC_GROUP;        // items whose loads are issued together
 constexpr int kDecMaxM = 64;                   // packets per launch (the host splits larger batches)
+#ifndef FC_SPARSE_MAXM
+#define FC_SPARSE_MAXM 128
+#endif
+// k_decode_sparse: packets per launch.  Every launch after the first re-reads and re-writes the
+// 4N-byte aggregate, so a whole 128-client batch is folded in one launch (uint8 fold counts
+// in cntC stay exact up to 255).
+constexpr int kSparseMaxM = FC_SPARSE_MAXM;
+static_assert(kSparseMaxM <= 255, "cntC counts are uint8");
 constexpr int kDecBlocksPerCU = 4;
 
 // Pointers read back from memory are generic (flat) to the compiler; loads through these
@@ -382,6 +390,9 @@ constexpr int kSR = 4;                         // entries per thread per item (1
 #ifndef FC_SGROUP
 #define FC_SGROUP 4
 #endif
+#ifndef FC_DEC_PIPE
+#define FC_DEC_PIPE 1
+#endif
 constexpr int kSGroup = FC_SGROUP;             // items whose loads are issued together
 constexpr int kSBlocksPerCU = 3;               // 41 KB LDS per workgroup
 
@@ -409,7 +420,7 @@ template <bool ACC>
 __global__ __launch_bounds__(kSBlock, kSBlocksPerCU) void k_decode_sparse(DecodeArgs a) {
   __shared__ __attribute__((aligned(16))) float tile[kChunk];
   __shared__ __attribute__((aligned(16))) uint8_t cntC[ACC ? kChunk : 16];   // poisoning folds
-  __shared__ SparseMeta s_meta[ACC ? kDecMaxM : 1];
+  __shared__ SparseMeta s_meta[ACC ? kSparseMaxM : 1];
   __shared__ uint32_t s_nC;
   const int tid = threadIdx.x;
   const uint32_t M = ACC ? (uint32_t)a.m : 1u;
@@ -483,6 +494,148 @@ __global__ __launch_bounds__(kSBlock, kSBlocksPerCU) void k_decode_sparse(Decode
   auto load_cnt = [&](uint32_t m, uint32_t c) -> uint32_t {     // uniform value, vector load
     return ((gu32*)uni_ptr(s_meta[m].cnt))[c];
   };
+#if FC_DEC_PIPE
+  // Two-slot software pipeline (loads issued in the order C0 C1 E0 | C2 E1 P0 | C3 E2 P1 ...,
+  // C = slot counts of a group of items, E = its entries, P = its fold): the entries of group
+  // g+1 are in flight while group g is folded, and every wait is a partial vmcnt (E_g is older
+  // than C_{g+2} and E_{g+1}).  Slots alternate by group parity, so nothing loaded is copied.
+  uint32_t gm[2][kSGroup], gc[2][kSGroup], cntg[2][kSGroup];
+  uint32_t ids_[2][kSGroup][kSR];
+  float vs_[2][kSGroup][kSR];
+  uint32_t cn_[2][kSGroup], im_[2][kSGroup], ic_[2][kSGroup];
+  auto issue_cnt = [&](int sl) {
+#pragma unroll
+    for (int d = 0; d < kSGroup; ++d) {
+      next_item(gm[sl][d], gc[sl][d]);
+      cntg[sl][d] = load_cnt(gm[sl][d], gc[sl][d]);
+    }
+  };
+  auto issue_ent = [&](int sl) {
+#pragma unroll
+    for (int d = 0; d < kSGroup; ++d) {
+      im_[sl][d] = gm[sl][d]; ic_[sl][d] = gc[sl][d];
+      const SparseMeta& pm = s_meta[im_[sl][d]];
+      const uint64_t lo = (uint64_t)ic_[sl][d] * kChunk;
+      gf32* val = (gf32*)uni_ptr(pm.val) + lo;
+      gu32* idx = (gu32*)uni_ptr(pm.idx) + lo;
+      cn_[sl][d] = uni32(cntg[sl][d]);
+      const uint32_t last = cn_[sl][d] ? cn_[sl][d] - 1 : 0u;
+#pragma unroll
+      for (int r = 0; r < kSR; ++r) {
+        const uint32_t e = min((uint32_t)(tid + r * kSBlock), last);
+        vs_[sl][d][r] = val[e];
+        ids_[sl][d][r] = idx[e];
+      }
+    }
+  };
+  auto process = [&](int sl, uint32_t t0) {
+    auto& ids = ids_[sl];
+    auto& vs = vs_[sl];
+    auto& cn = cn_[sl];
+    auto& im = im_[sl];
+    auto& ic = ic_[sl];
+#pragma unroll
+    for (int d = 0; d < kSGroup; ++d) {
+      const uint32_t t = t0 + d;
+      if (t >= T) break;                                         // uniform
+      const uint32_t m = im[d];
+      const uint32_t c = ic[d];
+      const uint64_t base = (uint64_t)c * kChunk;
+      const SparseMeta pm = s_meta[m];
+      const float w = __uint_as_float(uni32(__float_as_uint(pm.w)));
+      const uint64_t thresh = uni64(pm.thresh);
+      const uint32_t flags = uni32(pm.flags);
+      const uint32_t ib = flags & 0xffu, codec = (flags >> 8) & 0xffu;
+      const uint32_t key_mode = (flags >> 16) & 0xffu, poison = flags >> 24;
+      const bool scale = codec == FC_CODEC_DROPOUT_UNBIASED;     // fl32(fl64(g)/p), :60
+      const bool generic = scale || (key_mode == FC_KEY_PHILOX && thresh != 0);
+      auto fold = [&](uint32_t id, float v) {
+        const uint32_t loc = id - (uint32_t)base;
+        if (loc >= (uint32_t)kChunk) return;
+        if (ACC) {
+          const float term = __fmul_rn(v, w);
+          const float s2 = __fadd_rn(tile[loc], term);
+          tile[loc] = s2;
+          if (poison) cntC[loc] = (uint8_t)(cntC[loc] + 1u);
+        } else {
+          tile[loc] = v;
+        }
+      };
+      if (!generic) {                                            // top-k / dropout-biased
+        // a packet's locations are distinct: all tile reads first, then all writes (one LDS
+        // round trip per item, not one per entry)
+        uint32_t loc[kSR];
+        bool ok[kSR];
+        float tv[kSR];
+#pragma unroll
+        for (int r = 0; r < kSR; ++r) {
+          const uint32_t e = (uint32_t)(tid + r * kSBlock);
+          const uint32_t id = ids[d][r];
+          const bool keep = thresh == 0 || comp_of(mag_key(vs[d][r]), id, ib) >= thresh;
+          loc[r] = id - (uint32_t)base;
+          ok[r] = e < cn[d] && keep && loc[r] < (uint32_t)kChunk;
+          tv[r] = 0.f;
+          if (ACC && ok[r]) tv[r] = tile[loc[r]];
+        }
+#pragma unroll
+        for (int r = 0; r < kSR; ++r) {
+          if (!ok[r]) continue;
+          if (ACC) {
+            const float s2 = __fadd_rn(tv[r], __fmul_rn(vs[d][r], w));
+            tile[loc[r]] = s2;
+            if (poison) cntC[loc[r]] = (uint8_t)(cntC[loc[r]] + 1u);
+          } else {
+            tile[loc[r]] = vs[d][r];
+          }
+        }
+      } else {
+        const PktCache pk = meta_pkt_s(pm);
+        for (int r = 0; r < kSR; ++r) {
+          const uint32_t e = (uint32_t)(tid + r * kSBlock);
+          const uint32_t id = ids[d][r];
+          const float v = vs[d][r];
+          if (e < cn[d] && entry_kept(pk, id, v)) fold(id, scale ? (float)((double)v / pk.p) : v);
+        }
+      }
+      if (cn[d] > (uint32_t)(kSR * kSBlock)) {                   // dense slot (uniform, rare)
+        const PktCache pk = meta_pkt_s(pm);
+        gf32* pval = (gf32*)uni_ptr(pm.val) + base;
+        gu32* pidx = (gu32*)uni_ptr(pm.idx) + base;
+        for (uint32_t e = (uint32_t)(kSR * kSBlock + tid); e < cn[d]; e += kSBlock) {
+          const uint32_t id = pidx[e];
+          const float v = pval[e];
+          if (entry_kept(pk, id, v)) fold(id, scale ? (float)((double)v / pk.p) : v);
+        }
+        __builtin_amdgcn_s_waitcnt(0x0F70);                      // vmcnt(0): none left pending
+      }
+      __syncthreads();                                           // packet m folded
+      if (m + 1 == M) {                                          // chunk done
+        write_tile(c);
+        const uint32_t cnext = c + G;
+        if (t + 1 < T) {
+          __syncthreads();                                       // write-out read the tile
+          init_tile(cnext);
+          __syncthreads();
+        }
+      }
+    }
+  };
+  issue_cnt(0);
+  issue_cnt(1);
+  issue_ent(0);
+  init_tile(blockIdx.x);
+  __syncthreads();
+  for (uint32_t t0 = 0; t0 < T; t0 += 2 * kSGroup) {
+    issue_cnt(0);
+    issue_ent(1);
+    process(0, t0);
+    if (t0 + kSGroup >= T) break;                                 // uniform
+    issue_cnt(1);
+    issue_ent(0);
+    process(1, t0 + kSGroup);
+  }
+}
+#else
   uint32_t gm[kSGroup], gc[kSGroup], cntg[kSGroup];
 #pragma unroll
   for (int d = 0; d < kSGroup; ++d) {
@@ -604,6 +757,7 @@ __global__ __launch_bounds__(kSBlock, kSBlocksPerCU) void k_decode_sparse(Decode
     }
   }
 }
+#endif
 
 // Dense FedAVG over M row pointers (gar.py:44 with 'full' rows): one float4 per thread.
 __global__ __launch_bounds__(kBlock) void k_wsum(const float* const* rows, const float* w,

@@ -452,10 +452,11 @@ def test_fedavg_packets_signed_zeros_and_weight_classes(wkind):
         assert not (np.signbit(agg) & (agg == 0)).any()
 
 
-def test_fedavg_packets_signed_zeros_across_launches():
-    """> 64 packets: the sum continues across launches (acc_in), -0 bookkeeping included."""
+@pytest.mark.parametrize("M", [70, 129, 140])
+def test_fedavg_packets_signed_zeros_across_launches(M):
+    """> 128 packets: the sum continues across launches (acc_in), -0 bookkeeping included."""
     codec = _codec()
-    M, n, f = 70, 9_001, 0.5
+    n, f = 9_001, 0.5
     grads = _signed_zero_grads(M, n, np.random.default_rng(9))
     w = np.full(M, 1.0 / M, np.float32)
     k = co.num_kept(f, n)

@@ -1,4 +1,4 @@
+# A/B of k_decode_sparse<true> builds over 128 distinct 128 M-float top-k packets (one process each).
 set -e
-timeout -k 10 300 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/t.log 2>&1 || { tail -60 gpurun_out/t.log; exit 1; }
-tail -1 gpurun_out/t.log
-timeout -k 10 120 python tools/kbench.py --iters 5 --tag single
+timeout -k 10 180 python tools/kbench.py --dec 128 --iters 5 --tag m128
+timeout -k 10 180 python tools/kbench.py --lib tools/variants/lib_m64.so --dec 128 --iters 5 --tag m64

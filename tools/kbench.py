@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--tag", default="")
     ap.add_argument("--m", type=int, default=64)
     ap.add_argument("--batch", type=int, default=0)
+    ap.add_argument("--dec", type=int, default=0, help="FedAVG fold of this many DISTINCT packets")
     args = ap.parse_args()
     import torch
     from openmsftl_amd import _lib as L
@@ -30,6 +31,29 @@ def main():
     from openmsftl_amd import codec
     from openmsftl_amd.compression import kept_count
     n, k = args.n, kept_count(args.f, args.n)
+    if args.dec:                       # k_decode_sparse<true> over distinct packets (no cache reuse)
+        M = args.dec
+        gs = [torch.randn(n, device="cuda", generator=torch.Generator(device="cuda").manual_seed(s))
+              for s in range(M)]
+        pk = codec.encode_top_batch(gs, k)
+        codec.resolve(pk)
+        del gs
+        w = [1.0 / M] * M
+        views = codec.views_tensor(pk, w, torch.device("cuda"))
+        acc = torch.empty(n, device="cuda")
+        codec.decode_accumulate(pk, w, out=acc, views=views)
+        torch.cuda.synchronize()
+        with L.KernelTimer() as kt:
+            for _ in range(args.iters):
+                codec.decode_accumulate(pk, w, out=acc, views=views)
+            torch.cuda.synchronize()
+        us = kt.ms["decode"] * 1e3 / (args.iters * M)
+        ent = sum(int(p.n_entries) for p in pk) / M if hasattr(pk[0], "n_entries") else k
+        print(json.dumps({"tag": args.tag, "n": n, "k": k, "dec_packets": M,
+                          "dec_us_per_pkt": round(us, 2),
+                          "dec_GBps_8k": round(8.0 * k / (us * 1e-6) / 1e9, 1),
+                          "acc_sum": float(acc.double().sum())}), flush=True)
+        return
     if args.batch:                     # batched k_compact: clients per launch = --batch
         gs = [torch.randn(n, device="cuda", generator=torch.Generator(device="cuda").manual_seed(s))
               for s in range(args.batch)]
