@@ -213,6 +213,25 @@ def test_batch_encode_equals_single(n, f, M):
         _check_top_packet(x, k, pb, codec.decode(pb).cpu().numpy())
 
 
+@pytest.mark.parametrize("streams", [1, 2, 3])
+def test_batch_encode_forked_streams(streams):
+    """Sub-batches on forked streams (encode_top_batch(streams=...)) give the same packets as
+    one launch chain and as per-client encodes; odd M splits unevenly."""
+    codec = _codec()
+    n, M, f = 1 << 20, 5, 0.1
+    rng = np.random.default_rng(77)
+    host = [(rng.standard_normal(n) * 10.0 ** rng.uniform(-4, 1)).astype(np.float32)
+            for _ in range(M)]
+    grads = [torch.from_numpy(x).cuda() for x in host]
+    k = co.effective_k(co.num_kept(f, n), n)
+    batch = codec.encode_top_batch(grads, k, streams=streams)
+    torch.cuda.synchronize()
+    for x, g, pb in zip(host, grads, batch):
+        ps = codec.encode_top(g, k)
+        assert _packet_bytes(pb) == _packet_bytes(ps)
+        _check_top_packet(x, k, pb, codec.decode(pb).cpu().numpy())
+
+
 def test_batch_encode_philox_and_fallback():
     """Native rand-k keys per client (seed/offset per job) and one client whose sampled
     bracket misses (resolved by the per-packet exact path) inside the same batch."""

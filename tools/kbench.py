@@ -35,7 +35,7 @@ def main():
         M = args.dec
         gs = [torch.randn(n, device="cuda", generator=torch.Generator(device="cuda").manual_seed(s))
               for s in range(M)]
-        pk = codec.encode_top_batch(gs, k)
+        pk = codec.encode_top_batch(gs, k, streams=1)
         codec.resolve(pk)
         del gs
         w = [1.0 / M] * M
@@ -57,12 +57,12 @@ def main():
     if args.batch:                     # batched k_compact: clients per launch = --batch
         gs = [torch.randn(n, device="cuda", generator=torch.Generator(device="cuda").manual_seed(s))
               for s in range(args.batch)]
-        pk = codec.encode_top_batch(gs, k)
+        pk = codec.encode_top_batch(gs, k, streams=1)
         jobs = codec.encode_jobs(gs, pk)
         torch.cuda.synchronize()
         with L.KernelTimer() as kt:
             for _ in range(args.iters):
-                codec.encode_top_batch(gs, k, packets=pk, jobs=jobs, check=False)
+                codec.encode_top_batch(gs, k, packets=pk, jobs=jobs, check=False, streams=1)
             torch.cuda.synchronize()
         codec.resolve(pk)
         res = {c: round(kt.avg_us(c), 2) for c in L.TIME_CLASSES if kt.launches.get(c)}

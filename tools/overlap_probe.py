@@ -60,9 +60,26 @@ def main():
                                         views=views_g[g], continue_sum=g > 0)
         main_s.wait_stream(s_dec)
 
+    enc_streams = [torch.cuda.Stream(device=dev) for _ in range(G)]
+
+    def multistream():
+        """encode group g on its own stream (the latency-bound sample/resolve launches of one
+        group overlap the streaming compaction of another), then one fold on the main stream"""
+        main_s = torch.cuda.current_stream(dev)
+        ev0 = torch.cuda.Event()
+        ev0.record(main_s)
+        for g, gr in enumerate(groups):
+            enc_streams[g].wait_event(ev0)
+            with torch.cuda.stream(enc_streams[g]):
+                codec.encode_top_batch([grads[i] for i in gr], k, packets=[pkts[i] for i in gr],
+                                       jobs=jobs_g[g], check=False)
+        for st in enc_streams:
+            main_s.wait_stream(st)
+        codec.decode_accumulate(pkts, w, out=acc, views=views_all)
+
     res = {}
-    for name, fn in (("serial", serial), ("pipelined", pipelined), ("serial2", serial),
-                     ("pipelined2", pipelined)):
+    for name, fn in (("serial", serial), ("pipelined", pipelined), ("multistream", multistream),
+                     ("serial2", serial), ("multistream2", multistream)):
         fn()
         torch.cuda.synchronize()
         t0 = time.perf_counter()

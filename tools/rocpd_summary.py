@@ -20,7 +20,15 @@ import statistics
 
 
 def kernel_rows(db):
+    """(name, duration) per dispatch; the name carries the grid when rocpd records it, so
+    launches of one kernel with different batch shapes (grid.y = clients) are told apart."""
     c = sqlite3.connect(db)
+    cols = [r[1] for r in c.execute("pragma table_info(kernels)")]
+    gy = next((x for x in ("grid_size_y", "grid_y", "grid_size_y_") if x in cols), None)
+    gx = next((x for x in ("grid_size_x", "grid_x") if x in cols), None)
+    if gx and gy:
+        return [(f"{n} [grid {x}x{y}]", d) for n, d, x, y in
+                c.execute(f"select name, duration, {gx}, {gy} from kernels")]
     return c.execute("select name, duration from kernels").fetchall()
 
 
