@@ -824,10 +824,41 @@ __device__ __forceinline__ void compact_mag_item(const CompactArgs& a0, const Ma
 #ifndef FC_MAG1_WAVES_PER_EU
 #define FC_MAG1_WAVES_PER_EU 8
 #endif
+#ifndef FC_MAG1_IL
+#define FC_MAG1_IL 64
+#endif
+#ifndef FC_MAG1_ROT
+#define FC_MAG1_ROT 0
+#endif
+// Dispatch order: workgroups are dispatched x-fastest, so the linear id L = y*nch + x is
+// re-mapped to interleave the chunks of FC_MAG1_IL clients (chunk-major within a group of
+// clients): FC_MAG1_IL address streams are in flight at once instead of one.
+__device__ __forceinline__ void mag_item_of(uint32_t& client, uint32_t& chunk) {
+  if (FC_MAG1_IL == 1) {
+    client = blockIdx.y; chunk = blockIdx.x;
+    return;
+  }
+  const uint32_t nch = gridDim.x, M = gridDim.y;
+  const uint32_t L = blockIdx.y * nch + blockIdx.x;
+  const uint32_t gsz = nch * (uint32_t)FC_MAG1_IL;
+  const uint32_t g = L / gsz, r = L - g * gsz;
+  const uint32_t Ig = min((uint32_t)FC_MAG1_IL, M - g * (uint32_t)FC_MAG1_IL);
+  chunk = r / Ig;
+  const uint32_t j = r - chunk * Ig;
+  client = g * (uint32_t)FC_MAG1_IL + j;
+#if FC_MAG1_ROT
+  // client j of the group starts its walk j/Ig of the way through the gradient, so the
+  // concurrently read addresses of the group differ in their low bits too
+  chunk += (uint32_t)(((uint64_t)j * nch) / Ig);
+  if (chunk >= nch) chunk -= nch;
+#endif
+}
+
 template <int NW>
 __device__ __forceinline__ void compact_mag_wg(const CompactArgs& a0) {
   __shared__ __attribute__((aligned(16))) MagShared sh;
-  const uint32_t client = blockIdx.y, chunk = blockIdx.x;
+  uint32_t client, chunk;
+  mag_item_of(client, chunk);
   float x[MagGeo<NW>::kQ];
   mag_load<NW>(mag_g(a0, client), chunk, a0.n, x);       // g first, state behind it
   const MagState st = mag_state(mag_S(a0, client));
