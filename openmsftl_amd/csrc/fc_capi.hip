@@ -60,7 +60,7 @@ static WsPtrs ws_ptrs(void* ws, uint64_t n) {
 
 // Stratified sample + bracket ranks.  Full sample for n <= 1 M (exact bracket); otherwise
 // 64..1024 segments of 1024 (n/32 .. 1 M keys) and a +-6 sigma binomial margin.
-// Persistent decode grid: every workgroup resident (4 per CU at ~38 KiB LDS), each walking
+// Decode grid: per_cu workgroups per CU (capped at one per chunk), each walking
 // ceil(chunks / grid) chunks.  FC_DECODE_GRID overrides (tuning only).
 static uint32_t decode_grid(uint64_t n, uint32_t per_cu = kDecBlocksPerCU) {
   static const uint32_t forced = [] {
@@ -426,7 +426,9 @@ int fc_decode_dense(const fc_packet_view* pkt, int format, uint64_t n, void* out
   TimedLaunch t(FC_TIME_DECODE, s);
   if (format == FC_FMT_IDXVAL) {
     if (out_f64) hipLaunchKernelGGL((k_decode<FC_FMT_IDXVAL, false, true>), grid, blk, 0, s, a);
-    else hipLaunchKernelGGL(k_decode_sparse<false>, dim3(decode_grid(n, kSBlocksPerCU)), dim3(kSBlock), 0, s, a);
+    // dense decode: 4 resident WGs per CU (no fold counters in LDS); 1024 WGs measured 3 %
+    // faster than 768 and 14 % faster than one WG per chunk
+    else hipLaunchKernelGGL(k_decode_sparse<false>, dim3(decode_grid(n, 4)), dim3(kSBlock), 0, s, a);
   } else {
     if (out_f64) hipLaunchKernelGGL((k_decode<FC_FMT_BITMAP, false, true>), grid, blk, 0, s, a);
     else hipLaunchKernelGGL((k_decode<FC_FMT_BITMAP, false, false>), grid, blk, 0, s, a);
@@ -454,7 +456,9 @@ static int decode_accumulate(const fc_packet_view* views_dev, int m, int format,
     a.n = n; a.out = acc;
     TimedLaunch t(FC_TIME_DECODE, s);
     if (format == FC_FMT_IDXVAL)
-      hipLaunchKernelGGL(k_decode_sparse<true>, dim3(decode_grid(n, kSBlocksPerCU)), dim3(kSBlock), 0, s, a);
+      // fold: one WG per chunk (16384 at 128 M), not persistent: 23.4 -> 22.3 us per packet
+      // over 128 distinct packets (no tail of unequal per-WG chunk counts)
+      hipLaunchKernelGGL(k_decode_sparse<true>, dim3(decode_grid(n, 1u << 20)), dim3(kSBlock), 0, s, a);
     else hipLaunchKernelGGL((k_decode<FC_FMT_BITMAP, true, false>), grid, blk, 0, s, a);
     FC_LAUNCHED("k_decode(acc)");
   }

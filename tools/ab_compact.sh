@@ -1,6 +1,6 @@
-# A/B of sample sizes on the single-gradient path (one process each).
+# Dense decode grid A/B on the single-gradient path (FC_DECODE_GRID overrides the WG count).
 set -e
-timeout -k 10 120 python tools/kbench.py --iters 10 --tag single_s1024
-for V in s512 s256; do
-  timeout -k 10 120 python tools/kbench.py --lib tools/variants/lib_$V.so --iters 10 --tag single_$V
-done
+timeout -k 10 120 python tools/kbench.py --iters 10 --tag grid768
+FC_DECODE_GRID=1024 timeout -k 10 120 python tools/kbench.py --iters 10 --tag grid1024
+FC_DECODE_GRID=2048 timeout -k 10 120 python tools/kbench.py --iters 10 --tag grid2048
+FC_DECODE_GRID=16384 timeout -k 10 120 python tools/kbench.py --iters 10 --tag grid16384

@@ -1,5 +1,6 @@
-# A/B of k_decode_sparse<true> builds over 128 distinct 128 M-float top-k packets (one process each).
+# Fold grid A/B over 128 distinct 128 M-float top-k packets (FC_DECODE_GRID overrides the WG count).
 set -e
-for V in b64 occ4 occ3n b64; do
-  timeout -k 10 180 python tools/kbench.py --lib tools/variants/lib_$V.so --dec 128 --iters 5 --tag $V
+timeout -k 10 180 python tools/kbench.py --dec 128 --iters 5 --tag g768
+for G in 1536 4096 16384; do
+  FC_DECODE_GRID=$G timeout -k 10 180 python tools/kbench.py --dec 128 --iters 5 --tag g$G
 done
