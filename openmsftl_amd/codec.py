@@ -214,11 +214,12 @@ def encode_top_batch(grads: Sequence[torch.Tensor], k: int, *,
                      key_mode: int = L.FC_KEY_MAGNITUDE, seeds=None, offsets=None,
                      packets: Optional[Sequence[Packet]] = None,
                      jobs: Optional[torch.Tensor] = None, check: bool = True,
-                     streams: int = 2) -> list:
+                     streams: int = 2, groups: Optional[Sequence[int]] = None) -> list:
     """Top-k (or native rand-k) of M equal-length gradients in ONE launch per pipeline stage
     (fc_topk_encode_batch).  Same packets, bit for bit, as M calls of :func:`encode_top`.
     ``jobs``: a prebuilt :func:`encode_jobs` array for these exact grads/packets.
-    ``streams``: sub-batches launched on that many forked streams (joined before return)."""
+    ``streams``: sub-batches launched on that many forked streams (joined before return);
+    ``groups``: sub-batch sizes (default: ``streams`` equal parts), dealt to the streams in turn."""
     if not grads:
         raise ValueError("no gradients")
     lib = L.load()
@@ -246,32 +247,41 @@ def encode_top_batch(grads: Sequence[torch.Tensor], k: int, *,
         p._enc = (g, k, key_mode, s, o)
     if jobs is None:
         jobs = encode_jobs(grads, packets, seeds, offsets)
-    parts = max(1, min(int(streams), m, len(_side_streams(dev))))
-    if parts == 1:
+    nside = max(1, min(int(streams), m, len(_side_streams(dev))))
+    if groups is None:
+        groups = [(i + 1) * m // nside - i * m // nside for i in range(nside)]
+    groups = [int(x) for x in groups if int(x) > 0]
+    if sum(groups) != m:
+        raise ValueError(f"groups {groups} do not sum to {m} clients")
+    if nside == 1 or len(groups) == 1:
         ws = BatchWorkspace.get(n, m, dev)
         L.check(lib.fc_topk_encode_batch(_vp(jobs), m, n, k, key_mode, packets[0].capacity,
                                          _vp(ws.buf), ws.nbytes, _stream(dev)),
                 "fc_topk_encode_batch")
     else:
-        # Sub-batches on forked streams: one sub-batch's latency-bound sample/resolve launches
-        # run beside another's streaming k_compact_mag1 (measured 20.6 -> 19.4 ms for 128
-        # clients x 128 M, tools/overlap_probe.py).  Packets are identical; the caller's stream
-        # joins every fork before this returns, so later work (and frees) stay ordered.
+        # Sub-batches on forked streams (group i on stream i % streams): one sub-batch's
+        # latency-bound sample/resolve launches run beside another's streaming
+        # k_compact_mag1 (measured 20.6 -> 19.4 ms for 128 clients x 128 M,
+        # tools/overlap_probe.py).  Packets are identical; the caller's stream joins every
+        # fork before this returns, so later work (and frees) stay ordered.
         main = torch.cuda.current_stream(dev)
         fork = torch.cuda.Event()
         fork.record(main)
         job_bytes = ctypes.sizeof(L.EncodeJob)
         base = jobs.data_ptr()
-        for i, side in enumerate(_side_streams(dev)[:parts]):
-            lo, hi = i * m // parts, (i + 1) * m // parts
+        sides = _side_streams(dev)[:nside]
+        for side in sides:
             side.wait_event(fork)
-            with torch.cuda.stream(side):
-                ws = BatchWorkspace.get(n, hi - lo, dev)
-                L.check(lib.fc_topk_encode_batch(ctypes.c_void_p(base + lo * job_bytes), hi - lo,
+        lo = 0
+        for i, size in enumerate(groups):
+            with torch.cuda.stream(sides[i % nside]):
+                ws = BatchWorkspace.get(n, size, dev)
+                L.check(lib.fc_topk_encode_batch(ctypes.c_void_p(base + lo * job_bytes), size,
                                                  n, k, key_mode, packets[0].capacity,
                                                  _vp(ws.buf), ws.nbytes, _stream(dev)),
                         "fc_topk_encode_batch")
-        for side in _side_streams(dev)[:parts]:
+            lo += size
+        for side in sides:
             main.wait_stream(side)
     if check:
         resolve(packets)

@@ -213,8 +213,9 @@ def test_batch_encode_equals_single(n, f, M):
         _check_top_packet(x, k, pb, codec.decode(pb).cpu().numpy())
 
 
-@pytest.mark.parametrize("streams", [1, 2, 3])
-def test_batch_encode_forked_streams(streams):
+@pytest.mark.parametrize("streams,groups", [(1, None), (2, None), (3, None), (2, [1, 3, 1]),
+                                            (2, [4, 1])])
+def test_batch_encode_forked_streams(streams, groups):
     """Sub-batches on forked streams (encode_top_batch(streams=...)) give the same packets as
     one launch chain and as per-client encodes; odd M splits unevenly."""
     codec = _codec()
@@ -224,7 +225,7 @@ def test_batch_encode_forked_streams(streams):
             for _ in range(M)]
     grads = [torch.from_numpy(x).cuda() for x in host]
     k = co.effective_k(co.num_kept(f, n), n)
-    batch = codec.encode_top_batch(grads, k, streams=streams)
+    batch = codec.encode_top_batch(grads, k, streams=streams, groups=groups)
     torch.cuda.synchronize()
     for x, g, pb in zip(host, grads, batch):
         ps = codec.encode_top(g, k)
