@@ -250,9 +250,9 @@ def encode_top_batch(grads: Sequence[torch.Tensor], k: int, *,
     nside = max(1, min(int(streams), m, len(_side_streams(dev))))
     if groups is None:
         groups = [(i + 1) * m // nside - i * m // nside for i in range(nside)]
-    groups = [int(x) for x in groups if int(x) > 0]
-    if sum(groups) != m:
-        raise ValueError(f"groups {groups} do not sum to {m} clients")
+    groups = [int(x) for x in groups]
+    if any(x < 1 for x in groups) or sum(groups) != m:
+        raise ValueError(f"groups {groups} must be positive sizes summing to {m} clients")
     if nside == 1 or len(groups) == 1:
         ws = BatchWorkspace.get(n, m, dev)
         L.check(lib.fc_topk_encode_batch(_vp(jobs), m, n, k, key_mode, packets[0].capacity,
