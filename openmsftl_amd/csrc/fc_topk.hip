@@ -88,7 +88,13 @@ __device__ void bitonic_desc(uint64_t* sv, uint32_t P2) {
 // Sampling: level 1 (key >> 19, 4096 bins) and level 2 ((key >> 7) & 0xfff inside the two
 // level-1 bins that hold the bracket ranks).  Payload = global atomics only.
 // --------------------------------------------------------------------------------------
-constexpr int kSampleSegs = 4;   // segments per workgroup (grid = ceil(nseg / 4))
+#ifndef FC_SAMPLE_SEGS_PER_WG
+#define FC_SAMPLE_SEGS_PER_WG 4
+#endif
+// segments per workgroup (grid = ceil(nseg / 4)).  Measured per 128 M client (two launches):
+// 1 / 2 / 4 / 8 / 16 per WG = 65 / 50 / 45 / 47 / 60 us (more WGs: more histogram flush atomics;
+// fewer: less latency hiding).
+constexpr int kSampleSegs = FC_SAMPLE_SEGS_PER_WG;
 
 template <int KM, int LEVEL>
 __global__ __launch_bounds__(kBlock) void k_sample(const float* __restrict__ g, SamplePlan P,

@@ -1,6 +1,10 @@
-# A/B of k_compact_mag1 builds (one process each, 128 clients x 128 M per launch, one stream).
+# A/B of sample segments per workgroup (one process each): single 128 M gradient, 64-client batch.
 set -e
-timeout -k 10 120 python tools/kbench.py --batch 128 --iters 3 --tag il64
-for V in plain il128 w6; do
-  timeout -k 10 120 python tools/kbench.py --lib tools/variants/lib_$V.so --batch 128 --iters 3 --tag $V
+timeout -k 10 120 python tools/kbench.py --iters 10 --tag single_ss4
+for V in ss8 ss16; do
+  timeout -k 10 120 python tools/kbench.py --lib tools/variants/lib_$V.so --iters 10 --tag single_$V
+done
+timeout -k 10 120 python tools/kbench.py --batch 64 --iters 3 --tag b64_ss4
+for V in ss8 ss16; do
+  timeout -k 10 120 python tools/kbench.py --lib tools/variants/lib_$V.so --batch 64 --iters 3 --tag b64_$V
 done
