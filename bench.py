@@ -224,9 +224,15 @@ def main():
         extra["single_gradient"] = single_gradient(torch, codec, grads[0], k, n)
         extra["qsgd_single_gradient"] = qsgd_single(torch, codec, grads[0], n)
 
+    # the other named single-GPU sizes (BASELINE configs[1], configs[2]) as extras, after the
+    # headline workload's buffers are released
+    del grads, pkts, jobs, views, fold, hdrs
+    torch.cuda.empty_cache()
+    if world == 1 and rank == 0 and not args.no_single:
+        extra["configs_1_2"] = small_configs(torch, codec, L, device, f)
+
     cpu = None
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
-        del grads
         cpu = cpu_baseline(n, f)
 
     if rank == 0:
@@ -269,6 +275,41 @@ def single_gradient(torch, codec, g, k, n, iters=20):
             "grad_GBps": round(4.0 * n / dt / 1e9, 1),
             "alg_GBps": round(alg / dt / 1e9, 1),
             "hbm_frac": round(alg / dt / 1e9 / HBM_PEAK_GBPS, 4)}
+
+
+def small_configs(torch, codec, L, device, f, n=16_777_216, M=128, steps=5):
+    """BASELINE configs[1] (one 16 M gradient: encode + dense decode) and configs[2] (128
+    clients x 16 M: batched encode + on-device FedAVG fold), device-resident, same codec."""
+    from openmsftl_amd.compression import kept_count
+    k = kept_count(f, n)
+    grads = make_grads(M, n, 0, device, torch)
+    one = single_gradient(torch, codec, grads[0], k, n)
+    pkts = [codec.Packet.alloc(n, L.FC_FMT_IDXVAL, device, k=k) for _ in range(M)]
+    w = [1.0 / M] * M
+    jobs = codec.encode_jobs(grads, pkts)
+    views = codec.views_tensor(pkts, w, device)
+    acc = torch.empty(n, dtype=torch.float32, device=device)
+
+    def step():
+        codec.encode_top_batch(grads, k, packets=pkts, jobs=jobs, check=False)
+        codec.decode_accumulate(pkts, w, out=acc, views=views)
+
+    for _ in range(2):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    redo = codec.resolve(pkts)
+    alg = M * (4.0 * n + 16.0 * k) + 4.0 * n
+    return {"config1_single_16M": one,
+            "config2_128x16M": {"clients": M, "n": n, "k": k, "ms_per_step": round(dt * 1e3, 3),
+                                "grad_GBps": round(4.0 * n * M / dt / 1e9, 1),
+                                "alg_GBps": round(alg / dt / 1e9, 1),
+                                "hbm_frac": round(alg / dt / 1e9 / HBM_PEAK_GBPS, 4),
+                                "exact_fallbacks": redo}}
 
 
 def qsgd_single(torch, codec, g, n, bits=2, iters=20):
