@@ -185,14 +185,16 @@ class BatchWorkspace:
 
 
 _SIDE: dict = {}
+_MAX_SIDE = 4          # GPU_MAX_HW_QUEUES is 4: more forked streams would share queues
 
 
 def _side_streams(dev: torch.device, count: int = 2) -> list:
     """Forked streams for :func:`encode_top_batch` sub-batches (created once per device)."""
     key = dev.index if dev.index is not None else torch.cuda.current_device()
-    if key not in _SIDE:
-        _SIDE[key] = [torch.cuda.Stream(device=dev) for _ in range(count)]
-    return _SIDE[key]
+    lst = _SIDE.setdefault(key, [])
+    while len(lst) < count:
+        lst.append(torch.cuda.Stream(device=dev))
+    return lst[:count]
 
 
 def encode_jobs(grads: Sequence[torch.Tensor], packets: Sequence[Packet], seeds=None,
@@ -247,7 +249,7 @@ def encode_top_batch(grads: Sequence[torch.Tensor], k: int, *,
         p._enc = (g, k, key_mode, s, o)
     if jobs is None:
         jobs = encode_jobs(grads, packets, seeds, offsets)
-    nside = max(1, min(int(streams), m, len(_side_streams(dev))))
+    nside = max(1, min(int(streams), m, _MAX_SIDE))
     if groups is None:
         groups = [(i + 1) * m // nside - i * m // nside for i in range(nside)]
     groups = [int(x) for x in groups]
@@ -269,7 +271,7 @@ def encode_top_batch(grads: Sequence[torch.Tensor], k: int, *,
         fork.record(main)
         job_bytes = ctypes.sizeof(L.EncodeJob)
         base = jobs.data_ptr()
-        sides = _side_streams(dev)[:nside]
+        sides = _side_streams(dev, nside)
         for side in sides:
             side.wait_event(fork)
         lo = 0

@@ -13,9 +13,10 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-SPLITS = {"one": None, "2x64": [64, 64], "8-56-56-8": [8, 56, 56, 8],
-          "16-48-48-16": [16, 48, 48, 16], "4x32": [32, 32, 32, 32],
-          "16-56-56": [16, 56, 56], "8-60-60": [8, 60, 60]}
+SPLITS = {"one": (1, None), "2x64": (2, [64, 64]), "8-56-56-8": (2, [8, 56, 56, 8]),
+          "16-48-48-16": (2, [16, 48, 48, 16]), "4x32": (2, [32, 32, 32, 32]),
+          "4x32_4streams": (4, [32, 32, 32, 32]), "3 streams": (3, None),
+          "8x16_4streams": (4, [16] * 8)}
 
 
 def main():
@@ -40,10 +41,10 @@ def main():
     acc = torch.empty(n, dtype=torch.float32, device=dev)
     res, ref = {}, None
     for rep in range(2):
-        for name, groups in SPLITS.items():
+        for name, (nst, groups) in SPLITS.items():
             def step():
                 codec.encode_top_batch(grads, k, packets=pkts, jobs=jobs, check=False,
-                                       streams=1 if groups is None else 2, groups=groups)
+                                       streams=nst, groups=groups)
                 codec.decode_accumulate(pkts, w, out=acc, views=views)
             step()
             torch.cuda.synchronize()
