@@ -213,6 +213,24 @@ def test_batch_encode_equals_single(n, f, M):
         _check_top_packet(x, k, pb, codec.decode(pb).cpu().numpy())
 
 
+@pytest.mark.parametrize("M,n", [(65, 20_000), (70, 8_193 * 3), (130, 9_000)])
+def test_batch_encode_client_interleave(M, n):
+    """k_compact_mag1 interleaves the chunks of 64 clients in dispatch order: a full group, a
+    partial last group (M % 64 clients) and > 2 groups give the per-client packets."""
+    codec = _codec()
+    rng = np.random.default_rng(M * 7 + n)
+    host = [(rng.standard_normal(n) * 10.0 ** rng.uniform(-4, 1)).astype(np.float32)
+            for _ in range(M)]
+    grads = [torch.from_numpy(x).cuda() for x in host]
+    k = co.effective_k(co.num_kept(0.1, n), n)
+    batch = codec.encode_top_batch(grads, k, streams=1)
+    torch.cuda.synchronize()
+    for i in range(0, M, 7):
+        ps = codec.encode_top(grads[i], k)
+        assert _packet_bytes(batch[i]) == _packet_bytes(ps)
+        _check_top_packet(host[i], k, batch[i], codec.decode(batch[i]).cpu().numpy())
+
+
 @pytest.mark.parametrize("streams,groups", [(1, None), (2, None), (3, None), (2, [1, 3, 1]),
                                             (2, [4, 1])])
 def test_batch_encode_forked_streams(streams, groups):
