@@ -270,11 +270,24 @@ def single_gradient(torch, codec, g, k, n, iters=20):
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / iters
     codec.resolve([pkt])
+    # the same result through fc_topk_encode_dense (compaction streams q, fix-up of the slack)
+    for _ in range(3):
+        codec.compress_top_dense(g, k, out=out, packet=pkt, check=False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        codec.compress_top_dense(g, k, out=out, packet=pkt, check=False)
+    torch.cuda.synchronize()
+    dt_d = (time.perf_counter() - t0) / iters
+    codec.resolve([pkt])
     alg = 8.0 * n + 16.0 * k
     return {"n": n, "k": k, "us_per_encode_decode": round(dt * 1e6, 1),
             "grad_GBps": round(4.0 * n / dt / 1e9, 1),
             "alg_GBps": round(alg / dt / 1e9, 1),
-            "hbm_frac": round(alg / dt / 1e9 / HBM_PEAK_GBPS, 4)}
+            "hbm_frac": round(alg / dt / 1e9 / HBM_PEAK_GBPS, 4),
+            "fused_dense": {"us": round(dt_d * 1e6, 1),
+                            "alg_GBps": round(alg / dt_d / 1e9, 1),
+                            "hbm_frac": round(alg / dt_d / 1e9 / HBM_PEAK_GBPS, 4)}}
 
 
 def small_configs(torch, codec, L, device, f, n=16_777_216, M=128, steps=5):

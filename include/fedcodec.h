@@ -127,6 +127,15 @@ int fc_topk_encode(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_
                    uint64_t offset, uint32_t* idx, float* val, uint64_t capacity,
                    uint32_t* cnt, fc_packet_hdr* hdr, void* ws, size_t ws_bytes,
                    fc_stream_t stream);
+/* ---- top-k straight to the dense result (compression.py:31-37 returns q, not a packet) --
+ * The fc_topk_encode pipeline (magnitude keys) whose compaction pass also streams
+ * q = zeros_like(g); q[listed] = g into `dense` (n floats, 16-B aligned), then a fix-up
+ * launch zeroes the slack entries once T64 is known.  The packet is written as usual.  If the
+ * header reports FC_STATUS_RETRY_EXACT, `dense` is not valid: re-encode with
+ * fc_topk_encode_exact and fc_decode_dense (as for a packet).  Needs 0 < k < n. */
+int fc_topk_encode_dense(const float* g, uint64_t n, uint64_t k, uint32_t* idx, float* val,
+                         uint64_t capacity, uint32_t* cnt, fc_packet_hdr* hdr, void* ws,
+                         size_t ws_bytes, float* dense, fc_stream_t stream);
 /* ---- batched top-k / native rand-k: M clients, one launch per pipeline stage ----------
  * The same fast path as fc_topk_encode for m gradients of equal length n, with the grid's
  * y dimension indexing the client: 4 launches for the whole batch instead of 4 per client,

@@ -74,6 +74,8 @@ SIGNATURES = {
     "fc_workspace_init": (_i32, [_vp, _sz, _vp]),
     "fc_topk_encode": (_i32, [_vp, _u64, _u64, _i32, _u64, _u64, _vp, _vp, _u64, _vp, _vp,
                               _vp, _sz, _vp]),
+    "fc_topk_encode_dense": (_i32, [_vp, _u64, _u64, _vp, _vp, _u64, _vp, _vp, _vp, _sz, _vp,
+                                    _vp]),
     "fc_workspace_bytes_batch": (_sz, [_u64, _i32]),
     "fc_topk_encode_batch": (_i32, [_vp, _i32, _u64, _u64, _i32, _u64, _vp, _sz, _vp]),
     "fc_topk_encode_exact": (_i32, [_vp, _u64, _u64, _i32, _u64, _u64, _vp, _vp, _u64, _vp,

@@ -160,6 +160,38 @@ def encode_top(g: torch.Tensor, k: int, *, key_mode: int = L.FC_KEY_MAGNITUDE, s
     return packet
 
 
+def compress_top_dense(g: torch.Tensor, k: int, out: Optional[torch.Tensor] = None,
+                       packet: Optional[Packet] = None, check: bool = True) -> torch.Tensor:
+    """compression.py:31-37 on the device, straight to the dense q (fc_topk_encode_dense):
+    the compaction pass streams q while it lists the packet, a fix-up zeroes the slack.
+    Same bytes as ``decode(encode_top(g, k))``.  ``check=False`` skips the status read (call
+    :func:`resolve` + :func:`decode` yourself if the header reports a retry)."""
+    _require_cuda_f32(g)
+    n = g.numel()
+    if not 0 <= k <= n:
+        raise ValueError(f"k={k} outside [0, {n}]")
+    if out is None:
+        out = torch.empty(n, dtype=torch.float32, device=g.device)
+    _require_cuda_f32(out, "out")
+    if out.numel() != n:
+        raise ValueError("out must have n elements")
+    if packet is None:
+        packet = Packet.alloc(n, L.FC_FMT_IDXVAL, g.device, k=k)
+    if k == 0 or k >= n:                       # trivial thresholds: packet path
+        return decode(encode_top(g, k, packet=packet), out=out)
+    lib = L.load()
+    ws = Workspace.get(n, g.device)
+    packet.k = k
+    L.check(lib.fc_topk_encode_dense(_vp(g), n, k, _vp(packet.idx), _vp(packet.val),
+                                     packet.capacity, _vp(packet.cnt), _vp(packet.hdr),
+                                     _vp(ws.buf), ws.nbytes, _vp(out), _stream(g.device)),
+            "fc_topk_encode_dense")
+    packet._enc = (g, k, L.FC_KEY_MAGNITUDE, 0, 0)
+    if check and resolve([packet]):            # bracket missed: exact packet, then decode
+        decode(packet, out=out)
+    return out
+
+
 class BatchWorkspace:
     """Scratch for fc_topk_encode_batch: one encoder state per client (zeroed once)."""
 

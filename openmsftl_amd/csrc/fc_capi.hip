@@ -293,6 +293,46 @@ int fc_topk_encode(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_
   return launch_resolve(ra, s);
 }
 
+int fc_topk_encode_dense(const float* g, uint64_t n, uint64_t k, uint32_t* idx, float* val,
+                         uint64_t capacity, uint32_t* cnt, fc_packet_hdr* hdr, void* ws,
+                         size_t ws_bytes, float* dense, fc_stream_t stream) {
+  FC_CHECK(dense != nullptr, "dense is NULL");
+  FC_CHECK(((uintptr_t)dense & 15) == 0, "dense must be 16-byte aligned");
+  FC_CHECK(k > 0 && k < n, "fc_topk_encode_dense needs 0 < k < n (trivial k: encode + decode)");
+  CompactArgs ca; EngineArgs ea; ResolveArgs ra; HdrInit hi;
+  int rc = topk_args(g, n, k, FC_KEY_MAGNITUDE, 0, 0, idx, val, capacity, cnt, hdr, ws,
+                     ws_bytes, &ca, &ea, &ra, &hi);
+  if (rc) return rc;
+  ca.dense = dense;
+  hipStream_t s = (hipStream_t)stream;
+  const SamplePlan P = make_plan(n, k);
+  const uint32_t sgrid = (P.nseg + kSampleSegs - 1) / kSampleSegs;
+  {
+    TimedLaunch t(FC_TIME_SAMPLE, s);
+    hipLaunchKernelGGL((k_sample<kKeyMag, 1>), dim3(sgrid), dim3(kBlock), 0, s, g, P, 0ull, 0ull, ca.W, ca.ib, hdr, hi, nullptr, 0ull);
+    FC_LAUNCHED("k_sample1");
+    hipLaunchKernelGGL((k_sample<kKeyMag, 2>), dim3(sgrid), dim3(kBlock), 0, s, g, P, 0ull, 0ull, ca.W, ca.ib, hdr, hi, nullptr, 0ull);
+    FC_LAUNCHED("k_sample2");
+  }
+  {
+    TimedLaunch t(FC_TIME_COMPACT, s);
+    hipLaunchKernelGGL(k_compact_mag1_dense, dim3(ca.nchunks, 1), dim3(kCBlock), 0, s, ca);
+    FC_LAUNCHED("k_compact_mag1_dense");
+  }
+  rc = launch_resolve(ra, s);
+  if (rc) return rc;
+  DenseFixArgs fa;
+  fa.hdr = hdr; fa.idx = idx; fa.val = val; fa.cnt = cnt; fa.ccnt = ca.W.ccnt; fa.cand = ca.W.cand;
+  fa.dense = dense; fa.ib = ca.ib; fa.nchunks = ca.nchunks;
+  {
+    TimedLaunch t(FC_TIME_DECODE, s);
+    const uint32_t grid = ca.nchunks < 1024u ? ca.nchunks : 1024u;
+    hipLaunchKernelGGL(k_dense_fixup, dim3(grid), dim3(kBlock), 0, s, fa);
+    FC_LAUNCHED("k_dense_fixup");
+  }
+  return FC_OK;
+}
+
 size_t fc_workspace_bytes_batch(uint64_t n, int m) {
   return m > 0 ? (size_t)WsLayout::of(n).bytes * (size_t)m : 0;
 }

@@ -233,6 +233,7 @@ struct CompactArgs {
   HdrInit HI;
   const fc_encode_job* jobs;   // batched encode: client blockIdx.y overrides g / packet / W
   uint64_t ws_stride;
+  float* dense;             // fc_topk_encode_dense: also stream q = listed ? g : +0 (one client)
 };
 
 // Per-client fields of a batched launch (jobs[blockIdx.y]); no-op for a single client.
@@ -581,9 +582,10 @@ struct MagOut {
   uint64_t* cand;
   uint32_t* chist;
   uint32_t ib;
+  float* dense;             // nullptr unless fc_topk_encode_dense
 };
 
-template <bool FAST, typename SH, int NW>
+template <bool FAST, typename SH, int NW, bool DENSE = false>
 __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred& P,
                                                  float (&x)[MagGeo<NW>::kQ], SH& sh,
                                                  uint32_t chunk, uint32_t sbin, uint32_t par) {
@@ -632,12 +634,23 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
 
   // ---- phase 2: listed entries -> LDS stage (or straight to the slot when dense) -----------
   const uint64_t slot = base;
+  // fc_topk_encode_dense: the dense result q = zeros_like(g); q[listed] = g (compression.py:
+  // 33-37) leaves with the same coalesced layout as the loads; the slack entries (listed,
+  // comp < T64) are zeroed by k_dense_fixup once k_resolve has T64
+  auto dense_out = [&](int q, bool p) {
+    if (!DENSE) return;                               // uniform
+    const uint32_t e = base + FC_LOC(q);
+    if (!FAST && e >= P.n32) return;                    // partial last chunk
+    const float v = p ? (FAST ? x[q] : a.g[e]) : 0.0f;
+    __builtin_nontemporal_store(v, a.dense + e);
+  };
   if (tot_e <= (uint32_t)SH::kStageN) {                 // block-uniform
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const bool p = mag_listed<FAST>(P, x[q]);
       const uint32_t pos = prefix_count(__ballot(p)) + goff_of(q);
       if (p) sh.st[pos] = make_uint2(FC_LOC(q), __float_as_uint(FAST ? x[q] : a.g[base + FC_LOC(q)]));
+      dense_out(q, p);
     }
   } else {
 #pragma unroll
@@ -648,6 +661,7 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
         a.idx[slot + pos] = base + FC_LOC(q);
         a.val[slot + pos] = FAST ? x[q] : a.g[base + FC_LOC(q)];
       }
+      dense_out(q, p);
     }
   }
   // ---- candidates (rare; wave-uniform skip per group) ------------------------------------
@@ -741,6 +755,7 @@ __device__ __forceinline__ MagOut mag_out(const CompactArgs& a0, uint32_t client
   MagOut o;
   const WsPtrs W = a0.jobs ? ws_shift(a0.W, (uint64_t)client * a0.ws_stride) : a0.W;
   o.g = a0.g; o.idx = a0.idx; o.val = a0.val; o.cnt = a0.cnt;
+  o.dense = a0.jobs ? nullptr : a0.dense;
   if (a0.jobs) {                                // {g, idx, val, cnt} = first 32 B of the job
     const fc_u32x8 v = sload8(&a0.jobs[client]);
     o.g = as_ptr<const float>(v[0], v[1]); o.idx = as_ptr<uint32_t>(v[2], v[3]);
@@ -792,7 +807,7 @@ __device__ __forceinline__ void mag_load(const float* g, uint32_t chunk, uint64_
 // workgroups per CU overlap one another's load latency.  (A persistent variant that kept the
 // next item's loads in flight measured 1.3-2.5x SLOWER: hipcc spilled the second register set
 // and loop-carried state)
-template <int NW, typename SH>
+template <int NW, typename SH, bool DENSE = false>
 __device__ __forceinline__ void compact_mag_item(const CompactArgs& a0, const MagOut& o,
                                                  uint32_t chunk, const MagState& st,
                                                  float (&x)[MagGeo<NW>::kQ], SH& sh, uint32_t par) {
@@ -814,16 +829,19 @@ __device__ __forceinline__ void compact_mag_item(const CompactArgs& a0, const Ma
   P.cand_all = P.t_hi >= 0x7f800001u;
   P.T_hi = __uint_as_float(P.cand_all ? 0x7f800000u : P.t_hi);
   if (fast) {
-    compact_mag_body<true, SH, NW>(o, P, x, sh, chunk, st.sbin, par);
+    compact_mag_body<true, SH, NW, DENSE>(o, P, x, sh, chunk, st.sbin, par);
   } else if (none) {                                       // k = 0: nothing listed
     SH::barrier();
     if (tid == 0) {
       o.cnt[chunk] = 0;
       o.ccnt[chunk] = 0;
     }
+    if (DENSE)
+      for (uint32_t i = (uint32_t)tid; i < (uint32_t)kChunk && (uint64_t)base + i < a0.n; i += blockDim.x)
+        o.dense[base + i] = 0.0f;
   } else {                                                 // rare: exact integer predicate
     mag_exact_bits<NW>(P, x, base + (uint32_t)((tid >> 6) * 256 + lane_id()));
-    compact_mag_body<false, SH, NW>(o, P, x, sh, chunk, st.sbin, par);
+    compact_mag_body<false, SH, NW, DENSE>(o, P, x, sh, chunk, st.sbin, par);
   }
 }
 
@@ -863,7 +881,7 @@ __device__ __forceinline__ void mag_item_of(uint32_t& client, uint32_t& chunk) {
 #endif
 }
 
-template <int NW>
+template <int NW, bool DENSE = false>
 __device__ __forceinline__ void compact_mag_wg(const CompactArgs& a0) {
   __shared__ __attribute__((aligned(16))) MagShared sh;
   uint32_t client, chunk;
@@ -872,14 +890,59 @@ __device__ __forceinline__ void compact_mag_wg(const CompactArgs& a0) {
   mag_load<NW>(mag_g(a0, client), chunk, a0.n, x);       // g first, state behind it
   const MagState st = mag_state(mag_S(a0, client));
   if (threadIdx.x == 0) sh.ncand[0] = 0;
-  compact_mag_item<NW>(a0, mag_out(a0, client), chunk, st, x, sh, 0u);
+  compact_mag_item<NW, MagShared, DENSE>(a0, mag_out(a0, client), chunk, st, x, sh, 0u);
 }
 // 512 threads (8 waves x 16 elements per lane)
 __global__ __launch_bounds__(kCBlock, FC_MAG1_WAVES_PER_EU) void k_compact_mag1(CompactArgs a0) {
   compact_mag_wg<8>(a0);
 }
+// the same pass that also streams the dense result q (fc_topk_encode_dense; one client)
+__global__ __launch_bounds__(kCBlock, FC_MAG1_WAVES_PER_EU) void k_compact_mag1_dense(CompactArgs a0) {
+  compact_mag_wg<8, true>(a0);
+}
 // (A 256-thread form, 4 waves x 32 elements per lane, measured equal at 128 VGPRs and slower
 // with spills at 80-96: DESIGN.md §Lessons.)
+
+// --------------------------------------------------------------------------------------
+// k_dense_fixup (fc_topk_encode_dense, after k_resolve): k_compact_mag1 wrote q = g at every
+// listed element (comp >= L64); the slack ones (comp < T64) go back to +0.  Every slack entry
+// is a candidate (key <= t_hi), so each chunk's candidate slot holds them; a chunk whose
+// candidates overflowed that slot is re-checked from its packet entries (as k_resolve does).
+// A packet whose status is not OK is left alone: the host re-encodes it exactly and decodes.
+// --------------------------------------------------------------------------------------
+struct DenseFixArgs {
+  const fc_packet_hdr* hdr;
+  const uint32_t* idx;
+  const float* val;
+  const uint32_t* cnt;
+  const uint32_t* ccnt;
+  const uint64_t* cand;
+  float* dense;
+  uint32_t ib, nchunks;
+};
+
+__global__ __launch_bounds__(kBlock) void k_dense_fixup(DenseFixArgs a) {
+  if (ld_agent(&a.hdr->status) != FC_STATUS_OK) return;
+  const uint64_t T = ld_agent(&a.hdr->thresh);
+  const uint64_t imask = (1ull << a.ib) - 1;
+  for (uint32_t c = blockIdx.x; c < a.nchunks; c += gridDim.x) {
+    const uint32_t nc = a.ccnt[c];
+    if (nc == 0) continue;
+    if (nc <= (uint32_t)kCandSlot) {
+      for (uint32_t t = threadIdx.x; t < nc; t += blockDim.x) {
+        const uint64_t comp = a.cand[(uint64_t)c * kCandSlot + t];
+        if (comp < T) a.dense[comp & imask] = 0.0f;
+      }
+    } else {
+      const uint32_t ne = a.cnt[c];
+      for (uint32_t e = threadIdx.x; e < ne; e += blockDim.x) {
+        const uint32_t id = a.idx[(uint64_t)c * kChunk + e];
+        const float v = a.val[(uint64_t)c * kChunk + e];
+        if (comp_of(mag_key(v), id, a.ib) < T) a.dense[id] = 0.0f;
+      }
+    }
+  }
+}
 
 // --------------------------------------------------------------------------------------
 // k_resolve: exact T64 from the bracket's candidates (fast path, one launch).

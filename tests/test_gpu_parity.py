@@ -155,6 +155,71 @@ def test_top_bracket_miss_falls_back_to_exact():
     _check_top_packet(g, k, pkt, out)
 
 
+# ---- top straight to the dense q (fc_topk_encode_dense: compaction streams q + fix-up) ----
+def _dense_top(g_np, k):
+    codec = _codec()
+    gt = torch.from_numpy(g_np).cuda()
+    pkt = codec.Packet.alloc(g_np.shape[0], _L().FC_FMT_IDXVAL, gt.device, k=k)
+    q = codec.compress_top_dense(gt, k, packet=pkt).cpu().numpy()
+    return pkt, q
+
+
+@pytest.mark.parametrize("n", [5, 8192, 8193, 100_003, (1 << 20) + 17, 3_000_001])
+@pytest.mark.parametrize("f", [0.1, 0.01, 0.5, 0.999])
+def test_top_dense_sizes(n, f):
+    g = np.random.default_rng(n * 3 + int(f * 1000)).standard_normal(n, dtype=np.float32)
+    g *= np.float32(10.0) ** np.random.default_rng(n + 1).uniform(-4, 1, n).astype(np.float32)
+    k = co.effective_k(co.num_kept(f, n), n)
+    pkt, q = _dense_top(g, k)
+    _check_top_packet(g, k, pkt, q)
+
+
+@pytest.mark.parametrize("kind", sorted(ADVERSARIAL))
+def test_top_dense_adversarial(kind):
+    n, f = 2_500_000, 0.1
+    g = ADVERSARIAL[kind](n)
+    k = co.effective_k(co.num_kept(f, n), n)
+    pkt, q = _dense_top(g, k)
+    _check_top_packet(g, k, pkt, q)
+
+
+def test_top_dense_golden_and_bracket_miss():
+    """Reference goldens through the dense path, and a bracket miss (exact re-encode +
+    decode into the same output)."""
+    for name in G.cases("top__"):
+        m = G.meta(name)
+        g = G.input(name)
+        n = g.shape[0]
+        k = co.effective_k(co.num_kept(m["fraction"], n), n)
+        _, q = _dense_top(g.astype(np.float32), k)
+        ora = co.compress({"compression_function": "top", "fraction_coordinate": m["fraction"]}, g)
+        assert q.tobytes() == ora.astype(np.float32).tobytes(), name
+    n = 4 << 20
+    g = np.zeros(n, np.float32)
+    nseg = max(64, min(1024, n // 32 // 1024))
+    starts = ((np.arange(nseg, dtype=np.int64) * (n - 1024)) // (nseg - 1)) & ~3
+    sampled = np.zeros(n, bool)
+    for s in starts:
+        sampled[s:s + 1024] = True
+    hidden = np.nonzero(~sampled)[0]
+    g[hidden[: n // 8]] = np.random.default_rng(0).standard_normal(n // 8).astype(np.float32)
+    k = n // 10
+    pkt, q = _dense_top(g, k)
+    _check_top_packet(g, k, pkt, q)
+
+
+def test_top_dense_128M_equals_packet_decode():
+    """Size-independent check at the headline size: dense path == decode(encode_top)."""
+    codec = _codec()
+    n = 134_217_728
+    gt = torch.randn(n, device="cuda", generator=torch.Generator(device="cuda").manual_seed(5))
+    k = co.effective_k(co.num_kept(0.1, n), n)
+    q = codec.compress_top_dense(gt, k)
+    ref = codec.decode(codec.encode_top(gt, k))
+    assert torch.equal(q.view(torch.int32), ref.view(torch.int32))
+    assert int((q != 0).sum()) == k
+
+
 @pytest.mark.parametrize("key", sorted(G.manifest["large"]))
 def test_top_large_digests(key):
     d = G.manifest["large"][key]
