@@ -91,9 +91,10 @@ class Compression:
             if n == 0:
                 return grad.clone() if on_device else np.zeros_like(grad)
             g = self._to_device(grad)
-            if fn == 'top':
-                pkt = codec.encode_top(g, k)
-            elif host_idx is not None:
+            if fn == 'top':                    # q streamed by the compaction pass itself
+                out = codec.compress_top_dense(g, k)
+                return out if on_device else out.cpu().numpy()
+            if host_idx is not None:
                 mask = torch.from_numpy(bitmask_words(host_idx, n, False).view(np.int32)).to(g.device)
                 pkt = codec.encode_mask(g, L.FC_CODEC_RAND, mask_bits=mask, fmt=L.FC_FMT_IDXVAL)
             else:
