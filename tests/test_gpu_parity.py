@@ -137,7 +137,7 @@ def test_top_bracket_miss_falls_back_to_exact():
     """Large values hidden between the sampled segments -> bracket misses -> exact path."""
     n = 4 << 20
     g = np.zeros(n, np.float32)
-    nseg = max(64, min(1024, n // 32 // 1024))
+    nseg = max(64, min(1024, n // 64 // 1024))     # make_plan (fc_capi.hip)
     starts = ((np.arange(nseg, dtype=np.int64) * (n - 1024)) // (nseg - 1)) & ~3
     sampled = np.zeros(n, bool)
     for s in starts:
@@ -196,7 +196,7 @@ def test_top_dense_golden_and_bracket_miss():
         assert q.tobytes() == ora.astype(np.float32).tobytes(), name
     n = 4 << 20
     g = np.zeros(n, np.float32)
-    nseg = max(64, min(1024, n // 32 // 1024))
+    nseg = max(64, min(1024, n // 64 // 1024))     # make_plan (fc_capi.hip)
     starts = ((np.arange(nseg, dtype=np.int64) * (n - 1024)) // (nseg - 1)) & ~3
     sampled = np.zeros(n, bool)
     for s in starts:
@@ -332,7 +332,7 @@ def test_batch_encode_philox_and_fallback():
         want = po.selected_indices(keys, k)
         assert codec.decode(p).cpu().numpy().tobytes() == po.decode_dense(n, want, x[want]).tobytes()
     # hidden large values between sampled segments (as test_top_bracket_miss_falls_back_...)
-    nseg = max(64, min(1024, n // 32 // 1024))
+    nseg = max(64, min(1024, n // 64 // 1024))     # make_plan (fc_capi.hip)
     starts = ((np.arange(nseg, dtype=np.int64) * (n - 1024)) // (nseg - 1)) & ~3
     sampled = np.zeros(n, bool)
     for s in starts:
