@@ -1,6 +1,5 @@
-# Fold grid A/B over 128 distinct 128 M-float top-k packets (FC_DECODE_GRID overrides the WG count).
+# A/B of k_decode_sparse<true> builds over 128 distinct 128 M-float top-k packets (one process each).
 set -e
-timeout -k 10 180 python tools/kbench.py --dec 128 --iters 5 --tag g768
-for G in 1536 4096 16384; do
-  FC_DECODE_GRID=$G timeout -k 10 180 python tools/kbench.py --dec 128 --iters 5 --tag g$G
-done
+timeout -k 10 180 python tools/kbench.py --dec 128 --iters 5 --tag base
+timeout -k 10 180 python tools/kbench.py --lib tools/variants/lib_nt.so --dec 128 --iters 5 --tag nt
+timeout -k 10 180 python tools/kbench.py --dec 128 --iters 5 --tag base_again
