@@ -41,7 +41,7 @@ def parse():
     ap.add_argument("--fraction", type=float, default=0.1)
     ap.add_argument("--streams", type=int, default=2,
                     help="forked streams the batched encode is split over (1 = one launch chain)")
-    ap.add_argument("--roofline-steps", type=int, default=3,
+    ap.add_argument("--roofline-steps", type=int, default=5,
                     help="extra encode passes with one stream, timed per launch for `roofline`")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-single", action="store_true", help="skip the single-gradient probe")
