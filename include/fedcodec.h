@@ -232,6 +232,31 @@ int fc_qsgd_decode(const fc_packet_view* pkt, uint64_t n, float* out, fc_stream_
 int fc_qsgd_decode_accumulate(const fc_packet_view* views_dev, int m, uint64_t n, float* out,
                               int continue_sum, fc_stream_t stream);
 
+/* ---- float64 gradients ------------------------------------------------------------
+ * The reference reaches the codec with float64 gradients after RandomGaussian with
+ * noise_scale == 0 (attack_models.py:105-106); G takes that dtype (aggregation.py:61) and
+ * every codec and gar.py:44 then compute in float64.  These entry points produce the dense
+ * float64 result compress() returns (all buffers DEVICE, float64, 8-B aligned).
+ * fc_topk_dense_f64: 'top' (key_mode MAGNITUDE) / native 'rand' (PHILOX), exact radix select
+ *   of the k-th largest (key64 << 32 | idx) (<= 8 passes over g) then q = selected ? g : +0;
+ *   same tie rule as the fp32 path.  ws: fc_workspace_bytes(n), zeroed once.
+ * fc_mask_dense_f64: codec RAND (mask_bits required: q = keep ? g : +0), DROPOUT_BIASED
+ *   (q = g * keep) or DROPOUT_UNBIASED (q = (g * keep) / p), the reference's float64
+ *   arithmetic including -0 and NaN (inf * 0); mask_bits NULL = native Philox Bernoulli(p).
+ * fc_weighted_sum_dense_f64: gar.py:44 when G or the weights are float64: rows = DEVICE
+ *   array of m row pointers (float32 if rows_f64 == 0, promoted exactly), w = DEVICE
+ *   float64[m]; out = +0-started row-order fp64 sum of fl64(g_i * w_i); continue_sum != 0
+ *   continues the sum already in out.
+ * fc_div_scalar_f64: x = fl64(x / d) in place (np.mean's count division for float64 G). */
+int fc_topk_dense_f64(const double* g, uint64_t n, uint64_t k, int key_mode, uint64_t seed,
+                      uint64_t offset, double* out, void* ws, size_t ws_bytes,
+                      fc_stream_t stream);
+int fc_mask_dense_f64(const double* g, uint64_t n, int codec, const uint32_t* mask_bits, double p,
+                      uint64_t seed, uint64_t offset, double* out, fc_stream_t stream);
+int fc_weighted_sum_dense_f64(const void* const* rows, int rows_f64, const double* w, int m,
+                              uint64_t n, double* out, int continue_sum, fc_stream_t stream);
+int fc_div_scalar_f64(double* x, uint64_t n, double d, fc_stream_t stream);
+
 /* ---- measurement: HIP events around selected kernels, on the stream they run on -------
  * mask: FC_TIME_* bits.  Between fc_timing_begin and fc_timing_end every launch of a
  * selected kernel class is bracketed by a hipEvent pair; fc_timing_end synchronises those

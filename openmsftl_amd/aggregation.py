@@ -14,13 +14,20 @@ GAR (gar.py:44).  Here the rows never become a dense matrix on the common path:
   +0-started row-order sum ``np.mean`` computes) divided once by the row count
   (``fc_div_scalar``); later stages do the same over the dense merged rows
   (``fc_weighted_sum_dense``); the GAR then reduces the merged rows.
-* any other codec mix takes the generic path: the drop-in ``Compression`` per client in row
-  order (same NumPy RNG draws as the reference), rows stacked on the device, same reductions.
+* any other codec mix, float64 gradients (``RandomGaussian`` with ``noise_scale == 0``,
+  attack_models.py:105-106) and float64 GAR weights take the generic path: the drop-in
+  ``Compression`` per client in row order (same NumPy RNG draws as the reference), rows
+  stacked on the device in G's dtype, the same reductions in that dtype.
+
+``aggregate_grads`` is a plain function so that :func:`openmsftl_amd.integration.install` can
+bind it onto the REFERENCE ``Aggregator`` class (its ``self.gar`` may then be a reference GAR
+with no ``aggregate_packets``: G is then handed over as the host array the reference builds).
 
 Results are bit-exact against the reference (tests/golden/make_golden_agg.py pins the merge and
 the sign-of-zero semantics; tests/test_gpu_parity.py runs both paths).  Out of the hot path and
 not rebuilt: ``pc_analysis`` (randomized SVD of G), ``SpectralFedAvg``, ``update_model`` and the
-RL / DGA aggregators — they raise ``NotImplementedError``.
+RL / DGA aggregators: the device class raises ``NotImplementedError`` for them,
+the patched reference class keeps its own code for ``pc_analysis``.
 """
 from __future__ import annotations
 
@@ -42,6 +49,126 @@ def _cluster_bounds(m: int, cluster_size: int):
     if bounds[-1][1] < m:
         bounds[-1][1] = m
     return bounds
+
+
+def _device_of(agg) -> torch.device:
+    dev = getattr(agg, "device", None)
+    if isinstance(dev, torch.device) and dev.type == "cuda":
+        return dev
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def common_top_fraction(clients) -> Optional[float]:
+    """The fraction when every client compresses with 'top' at one fraction whose k lies in
+    [0, N] (f < 0 / f > 1 keep the reference's slice semantics: generic path), else None."""
+    fr = None
+    for c in clients:
+        C = c.C
+        if getattr(C, "compression_function", None) != "top":
+            return None
+        f = C.fraction_coordinates
+        if fr is None:
+            fr = f
+        elif f != fr:
+            return None
+    n = len(clients[0].grad)
+    return fr if 0 <= kept_count(fr, n) <= n else None
+
+
+def encode_top_clients(clients, n: int, f: float, device: torch.device):
+    """Every client's top-k packet (one batched launch sequence; exact re-encode of the rare
+    RETRY packets).  The packets drop their reference to the device gradient afterwards."""
+    k = kept_count(f, n)
+    grads = [torch.from_numpy(np.ascontiguousarray(c.grad)).to(device, non_blocking=True)
+             for c in clients]
+    if 0 < k < n:
+        packets = codec.encode_top_batch(grads, k)
+    else:                                   # trivial k (0, all, or the negative slice)
+        packets = [codec.encode_top(g, k) for g in grads]
+    for p in packets:                       # resolved: the gradient is no longer needed
+        p.release()
+    return packets
+
+
+def merge_packets(packets, cluster_size: int) -> torch.Tensor:
+    """First merge stage straight from the packets (aggregation.py:80-93).  Merged rows are
+    separate (16-B aligned) buffers while they are written, stacked at the end."""
+    bounds = _cluster_bounds(len(packets), cluster_size)
+    rows = []
+    for s, e in bounds:
+        r = codec.decode_accumulate(packets[s:e], [1.0] * (e - s))
+        rows.append(codec.div_scalar(r, float(e - s)))
+    return torch.stack(rows)
+
+
+def merge_stages(G: torch.Tensor, sizes) -> torch.Tensor:
+    """Merge stages over dense device rows (fp32 or fp64 G): +0-started sums (weights 1),
+    then / count, in G's dtype (np.mean(G[s:e], axis=0), aggregation.py:91)."""
+    for cs in sizes:
+        bounds = _cluster_bounds(G.shape[0], cs)
+        rows = []
+        for s, e in bounds:
+            r = codec.weighted_sum_dense(G[s:e], torch.ones(e - s, dtype=G.dtype), out_dtype=G.dtype)
+            rows.append(codec.div_scalar(r, float(e - s)))
+        G = torch.stack(rows)
+    return G
+
+
+def aggregate_grads(self, clients: List, input_feature: np.ndarray = None,
+                    val_loader=None) -> None:
+    """aggregation.py:54-78 on the device: sets ``self.agg_grad`` (host array) and
+    ``self.curr_G`` as the reference does."""
+    if len(clients) == 0:
+        raise Exception('Client List is Empty')
+    self.curr_packets = None                # last round's packets go before this round encodes
+    if self.analyze_pc is True:
+        ref = getattr(type(self), "_ref_aggregate_grads", None)
+        if ref is not None:                 # patched reference class: its own SVD analysis
+            return ref(self, clients, input_feature, val_loader)
+        raise NotImplementedError("pc_analysis (randomized SVD of G) is outside the hot path")
+    dev = _device_of(self)
+    grad0 = np.asarray(clients[0].grad)
+    n = grad0.shape[0]
+    if any(np.asarray(c.grad).shape != (n,) for c in clients):
+        raise ValueError("client gradients must share one length (aggregation.py:61)")
+    device_gar = hasattr(self.gar, "aggregate_packets")
+    w = getattr(self.gar, "gradient_weights", None)
+    f32_weights = w is None or np.asarray(w).dtype == np.float32
+    top_f = None
+    if device_gar and grad0.dtype == np.float32 and f32_weights:
+        top_f = common_top_fraction(clients)
+    if top_f is not None:
+        packets = encode_top_clients(clients, n, top_f, dev)
+        self.curr_packets = packets
+        if self.num_hierarchies > 0:
+            H = merge_packets(packets, self.cluster_size_list[0])
+            H = merge_stages(H, self.cluster_size_list[1:])
+            self.curr_G = H
+            agg = self.gar.aggregate(G=H, client_ids=np.arange(H.shape[0]))
+        else:
+            self.curr_G = None
+            agg = self.gar.aggregate_packets(packets)
+    else:
+        # generic codec mix / float64: the drop-in Compression per client, in row order; rows
+        # take G's dtype (aggregation.py:61-63: G = zeros(..., dtype=clients[0].grad.dtype))
+        tdt = torch.float64 if grad0.dtype == np.float64 else torch.float32
+        G = torch.empty((len(clients), n), dtype=tdt, device=dev)
+        for ix, c in enumerate(clients):
+            q = c.C.compress(c.grad)
+            q = q if isinstance(q, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(q))
+            G[ix].copy_(q)                  # implicit cast to G's dtype, as G[ix, :] = q
+        if self.num_hierarchies > 0:
+            G = merge_stages(G, self.cluster_size_list)
+            client_ids = np.arange(G.shape[0])
+        else:
+            client_ids = np.array([c.client_id for c in clients])
+        if device_gar:
+            self.curr_G = G
+            agg = self.gar.aggregate(G=G, client_ids=client_ids)
+        else:                               # a reference GAR: the host G it expects
+            self.curr_G = G.cpu().numpy()
+            agg = self.gar.aggregate(G=self.curr_G, client_ids=client_ids)
+    self.agg_grad = agg.cpu().numpy() if isinstance(agg, torch.Tensor) else agg
 
 
 class Aggregator:
@@ -66,7 +193,7 @@ class Aggregator:
         self.cluster_size_list = self.aggregation_config.get("cluster_size_list", [])
         assert self.num_hierarchies == len(self.cluster_size_list), \
             "Unmatched hierarchial and cluster size list length"
-        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        self.device = device                # None: the current device, resolved per call
 
     def __get_gar(self):                                                  # aggregation.py:44-52
         scheme = self.aggregation_config["aggregation_scheme"]
@@ -76,97 +203,10 @@ class Aggregator:
             raise NotImplementedError("SpectralFedAvg is outside the codec hot path (DESIGN.md §8)")
         raise NotImplementedError
 
-    # ---- aggregation.py:54-78 ---------------------------------------------------------------
-    def aggregate_grads(self, clients: List, input_feature: np.ndarray = None,
-                        val_loader=None) -> None:
-        if len(clients) == 0:
-            raise Exception('Client List is Empty')
-        if self.analyze_pc is True:
-            raise NotImplementedError("pc_analysis (randomized SVD of G) is outside the hot path")
-        grad0 = np.asarray(clients[0].grad)
-        if grad0.dtype != np.float32:
-            raise TypeError("device aggregation handles float32 gradients (DESIGN.md §8)")
-        n = grad0.shape[0]
-        if any(np.asarray(c.grad).shape != (n,) for c in clients):
-            raise ValueError("client gradients must share one length (aggregation.py:61)")
-        top_f = self._common_top_fraction(clients)
-        if top_f is not None:
-            packets = self._encode_top(clients, n, top_f)
-            self.curr_packets = packets
-            if self.num_hierarchies > 0:
-                H = self._merge_packets(packets, self.cluster_size_list[0])
-                H = self._merge_stages(H, self.cluster_size_list[1:])
-                self.curr_G = H
-                agg = self.gar.aggregate(G=H, client_ids=np.arange(H.shape[0]))
-            else:
-                self.curr_G = None
-                agg = self.gar.aggregate_packets(packets)
-        else:
-            # generic codec mix: the drop-in Compression per client, in row order
-            rows = [torch.from_numpy(np.ascontiguousarray(c.C.compress(c.grad), dtype=np.float32))
-                    for c in clients]
-            G = torch.stack(rows).to(self.device)
-            self.curr_packets = None
-            if self.num_hierarchies > 0:
-                G = self._merge_stages(G, self.cluster_size_list)
-                client_ids = np.arange(G.shape[0])
-            else:
-                client_ids = np.array([c.client_id for c in clients])
-            self.curr_G = G
-            agg = self.gar.aggregate(G=G, client_ids=client_ids)
-        self.agg_grad = agg.cpu().numpy() if isinstance(agg, torch.Tensor) else agg
-
-    # ---- helpers ----------------------------------------------------------------------------
-    @staticmethod
-    def _common_top_fraction(clients) -> Optional[float]:
-        """The fraction when every client compresses with 'top' at one fraction whose k lies in
-        [0, N] (f < 0 / f > 1 keep the reference's slice semantics: generic path), else None."""
-        fr = None
-        for c in clients:
-            C = c.C
-            if getattr(C, "compression_function", None) != "top":
-                return None
-            f = C.fraction_coordinates
-            if fr is None:
-                fr = f
-            elif f != fr:
-                return None
-        n = len(clients[0].grad)
-        return fr if 0 <= kept_count(fr, n) <= n else None
-
-    def _encode_top(self, clients, n: int, f: float):
-        k = kept_count(f, n)
-        grads = [torch.from_numpy(np.ascontiguousarray(c.grad)).to(self.device, non_blocking=True)
-                 for c in clients]
-        if 0 < k < n:
-            packets = codec.encode_top_batch(grads, k)
-        else:                                   # trivial k (0, all, or the negative slice)
-            packets = [codec.encode_top(g, k) for g in grads]
-        return packets
-
-    def _merge_packets(self, packets, cluster_size: int) -> torch.Tensor:
-        """First merge stage straight from the packets (aggregation.py:80-93).  Merged rows are
-        separate (16-B aligned) buffers while they are written, stacked at the end."""
-        bounds = _cluster_bounds(len(packets), cluster_size)
-        rows = []
-        for s, e in bounds:
-            r = codec.decode_accumulate(packets[s:e], [1.0] * (e - s))
-            rows.append(codec.div_scalar(r, float(e - s)))
-        return torch.stack(rows)
-
-    def _merge_stages(self, G: torch.Tensor, sizes) -> torch.Tensor:
-        """Later merge stages over dense device rows: +0-started sums (weights 1), then / count."""
-        for cs in sizes:
-            bounds = _cluster_bounds(G.shape[0], cs)
-            rows = []
-            for s, e in bounds:
-                r = codec.weighted_sum_dense(G[s:e], torch.ones(e - s, dtype=torch.float32))
-                rows.append(codec.div_scalar(r, float(e - s)))
-            G = torch.stack(rows)
-        return G
+    aggregate_grads = aggregate_grads
 
     def update_model(self):
         raise NotImplementedError("model update is outside the codec hot path (DESIGN.md §8)")
 
 
-__all__ = ["Aggregator", "Compression"]
+__all__ = ["Aggregator", "Compression", "aggregate_grads"]

@@ -32,11 +32,11 @@ def _stream(device=None):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
-def _require_cuda_f32(g: torch.Tensor, name="g", align: int = 16):
+def _require_cuda_f32(g: torch.Tensor, name="g", align: int = 16, dtype=torch.float32):
     if not isinstance(g, torch.Tensor) or not g.is_cuda:
         raise TypeError(f"{name} must be a CUDA (HIP) tensor")
-    if g.dtype != torch.float32:
-        raise TypeError(f"{name} must be float32 (got {g.dtype}); the HIP codec is fp32-only")
+    if g.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype} (got {g.dtype})")
     if g.dim() != 1 or not g.is_contiguous():
         raise ValueError(f"{name} must be a contiguous 1-D tensor")
     if g.data_ptr() % align:
@@ -99,6 +99,11 @@ class Packet:
     def capacity(self) -> int:
         return self.val.numel()
 
+    def release(self) -> None:
+        """Drop the reference to the source gradient kept for the exact re-encode (call once
+        :func:`resolve` has seen the packet OK), so the gradient's memory can be reused."""
+        self._enc = None
+
     def view(self, weight: float = 1.0) -> L.PacketView:
         return L.PacketView(idx=self.idx.data_ptr() if self.idx is not None else 0,
                             val=self.val.data_ptr(),
@@ -128,8 +133,11 @@ class Packet:
 
 
 def headers(packets: Sequence[Packet]) -> list:
-    """Read many device headers with one synchronising copy when they share storage."""
-    return [p.header() for p in packets]
+    """Read many device headers with ONE synchronising copy (stacked on the device first)."""
+    if not packets:
+        return []
+    raw = torch.stack([p.hdr for p in packets]).cpu().numpy()
+    return [L.PacketHdr.from_buffer_copy(raw[i].tobytes()) for i in range(len(packets))]
 
 
 # ---------------------------------------------------------------------------------------
@@ -327,11 +335,10 @@ def resolve(packets: Sequence[Packet]) -> int:
     Returns the number of packets that needed the exact path."""
     lib = L.load()
     redo = 0
-    for p in packets:
-        h = p.header()
+    for p, h in zip(packets, headers(packets)):       # one sync for the whole batch
         if h.status == L.FC_STATUS_OK:
             continue
-        if h.status != L.FC_STATUS_RETRY_EXACT or not hasattr(p, "_enc"):
+        if h.status != L.FC_STATUS_RETRY_EXACT or getattr(p, "_enc", None) is None:
             raise L.FedCodecError(f"packet status {h.status}")
         g, k, key_mode, seed, offset = p._enc
         ws = Workspace.get(g.numel(), g.device)
@@ -419,32 +426,97 @@ def decode_accumulate(packets: Sequence[Packet], weights, out: Optional[torch.Te
     return out
 
 
-def weighted_sum_dense(rows, weights: torch.Tensor, out: Optional[torch.Tensor] = None):
-    """gar.py:44 on dense device rows (a (M, N) tensor or a list of 1-D tensors)."""
+def weighted_sum_dense(rows, weights: torch.Tensor, out: Optional[torch.Tensor] = None,
+                       out_dtype: Optional[torch.dtype] = None, continue_sum: bool = False):
+    """gar.py:44 on dense device rows (a (M, N) tensor or a list of 1-D tensors).
+
+    float32 rows and float32 weights: fp32 arithmetic (k_wsum).  Anything float64 (rows,
+    weights or ``out_dtype``): NumPy's promotion of ``G * w`` to float64, fp64 arithmetic
+    (k_wsum64); the result is float64."""
     lib = L.load()
     if isinstance(rows, torch.Tensor):
         rows = list(rows.unbind(0))
+    rdt = rows[0].dtype
+    if rdt not in (torch.float32, torch.float64) or any(r.dtype != rdt for r in rows):
+        raise TypeError("rows must all be float32 or all float64")
+    f64 = rdt == torch.float64 or weights.dtype == torch.float64 or out_dtype == torch.float64
     for r in rows:
-        _require_cuda_f32(r, "row", align=4)
+        _require_cuda_f32(r, "row", align=4 if rdt == torch.float32 else 8, dtype=rdt)
     n, dev = rows[0].numel(), rows[0].device
     if any(r.numel() != n for r in rows):
         raise ValueError("rows must have equal length")
-    w = weights.to(device=dev, dtype=torch.float32).contiguous()
     ptrs = torch.tensor([r.data_ptr() for r in rows], dtype=torch.int64).to(dev)
+    odt = torch.float64 if f64 else torch.float32
     if out is None:
-        out = torch.empty(n, dtype=torch.float32, device=dev)
+        if continue_sum:
+            raise ValueError("continue_sum needs the partial sum in `out`")
+        out = torch.empty(n, dtype=odt, device=dev)
+    if out.dtype != odt or out.numel() != n or not out.is_cuda:
+        raise ValueError(f"out must be a CUDA {odt} tensor of {n} elements")
+    if f64:
+        w = weights.to(device=dev, dtype=torch.float64).contiguous()   # exact for fp32 weights
+        L.check(lib.fc_weighted_sum_dense_f64(_vp(ptrs), int(rdt == torch.float64), _vp(w),
+                                              len(rows), n, _vp(out), int(continue_sum),
+                                              _stream(dev)), "fc_weighted_sum_dense_f64")
+        return out
+    if continue_sum:
+        raise ValueError("continue_sum is a float64-path option")
+    w = weights.to(device=dev, dtype=torch.float32).contiguous()
     L.check(lib.fc_weighted_sum_dense(_vp(ptrs), _vp(w), len(rows), n, _vp(out), _stream(dev)),
             "fc_weighted_sum_dense")
     return out
 
 
 def div_scalar(x: torch.Tensor, d: float) -> torch.Tensor:
-    """x = fl(x / d) in place (fp32 division; the count division of np.mean, aggregation.py:91)."""
+    """x = fl(x / d) in place, in x's dtype (the count division of np.mean, aggregation.py:91)."""
     lib = L.load()
+    if x.dtype == torch.float64:
+        _require_cuda_f32(x, "x", align=8, dtype=torch.float64)
+        L.check(lib.fc_div_scalar_f64(_vp(x), x.numel(), float(d), _stream(x.device)),
+                "fc_div_scalar_f64")
+        return x
     _require_cuda_f32(x, "x")
     L.check(lib.fc_div_scalar(_vp(x), x.numel(), ctypes.c_float(d), _stream(x.device)),
             "fc_div_scalar")
     return x
+
+
+# ---- float64 gradients (attack_models.py:105-106 -> aggregation.py:61) ----------------------
+def compress_top_dense_f64(g: torch.Tensor, k: int, *, key_mode: int = L.FC_KEY_MAGNITUDE,
+                           seed: int = 0, offset: int = 0,
+                           out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """compression.py:31-37 ('top') / native 'rand' (PHILOX keys) on a float64 gradient: the
+    dense float64 q (fc_topk_dense_f64, exact radix select; same tie rule as fp32)."""
+    _require_cuda_f32(g, align=8, dtype=torch.float64)
+    n = g.numel()
+    if not 0 <= k <= n:
+        raise ValueError(f"k={k} outside [0, {n}]")
+    if out is None:
+        out = torch.empty(n, dtype=torch.float64, device=g.device)
+    _require_cuda_f32(out, "out", align=8, dtype=torch.float64)
+    lib = L.load()
+    ws = Workspace.get(n, g.device)
+    L.check(lib.fc_topk_dense_f64(_vp(g), n, k, key_mode, seed, offset, _vp(out), _vp(ws.buf),
+                                  ws.nbytes, _stream(g.device)), "fc_topk_dense_f64")
+    return out
+
+
+def mask_dense_f64(g: torch.Tensor, codec: int, *, p: float = 0.5,
+                   mask_bits: Optional[torch.Tensor] = None, seed: int = 0, offset: int = 0,
+                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """'rand' (host permutation mask) and 'dropout-*' on a float64 gradient, with the
+    reference's float64 arithmetic (g * mask, (g * mask) / p): fc_mask_dense_f64."""
+    _require_cuda_f32(g, align=8, dtype=torch.float64)
+    n = g.numel()
+    if mask_bits is not None and (mask_bits.dtype != _U32 or not mask_bits.is_cuda
+                                  or mask_bits.numel() * 32 < n):
+        raise ValueError("mask_bits must be an int32 CUDA tensor of ceil(n/32) words")
+    if out is None:
+        out = torch.empty(n, dtype=torch.float64, device=g.device)
+    lib = L.load()
+    L.check(lib.fc_mask_dense_f64(_vp(g), n, codec, _vp(mask_bits), float(p), seed, offset,
+                                  _vp(out), _stream(g.device)), "fc_mask_dense_f64")
+    return out
 
 
 # ---- QSGD (compression.py:62-74; opt-in, parity unpinned: oracle/qsgd_oracle.py) ----------
@@ -486,7 +558,8 @@ def encode_qsgd(g: torch.Tensor, bits: int, *, seed: int = 0, offset: int = 0,
     n, dev = g.numel(), g.device
     if packet is None:
         packet = QsgdPacket.alloc(n, bits, dev)
-    key = (dev.index,)
+    key = (dev.index if dev.index is not None else torch.cuda.current_device(),
+           torch.cuda.current_stream(dev).cuda_stream)        # k_qsgd_norm's ticket: per stream
     ws = _QSGD_WS.get(key)
     if ws is None:
         ws = _QSGD_WS[key] = torch.zeros(int(lib.fc_qsgd_workspace_bytes()), dtype=torch.uint8,

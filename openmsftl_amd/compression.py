@@ -16,7 +16,10 @@ mask/index set crosses to the GPU.  ``'rng': 'philox'`` draws on the device inst
 stream-identical to the reference (documented in DESIGN.md).
 
 Inputs: 1-D float32 NumPy arrays (the reference's `client.grad`, client.py:53) or 1-D
-float32 CUDA tensors (device-resident; the result is then a CUDA tensor).
+float32 CUDA tensors (device-resident; the result is then a CUDA tensor).  float64 gradients
+(what ``RandomGaussian`` with ``noise_scale == 0`` hands over, attack_models.py:105-106) run
+on the float64 kernels and return float64, as the reference does; for them 'dropout-*' keeps
+the reference's exact g * 0 (including -0.0).
 
 Deliberate, documented deviations:
   * ties in 'top' are broken highest-index-first (= stable argsort reversed); the
@@ -91,6 +94,16 @@ class Compression:
             if n == 0:
                 return grad.clone() if on_device else np.zeros_like(grad)
             g = self._to_device(grad)
+            if g.dtype == torch.float64:       # float64 kernels (exact radix select / mask)
+                if fn == 'top':
+                    out = codec.compress_top_dense_f64(g, k)
+                elif host_idx is not None:
+                    mask = torch.from_numpy(bitmask_words(host_idx, n, False).view(np.int32)).to(g.device)
+                    out = codec.mask_dense_f64(g, L.FC_CODEC_RAND, mask_bits=mask)
+                else:
+                    out = codec.compress_top_dense_f64(g, k, key_mode=L.FC_KEY_PHILOX, seed=self.seed,
+                                                       offset=self._next_offset())
+                return out if on_device else out.cpu().numpy()
             if fn == 'top':                    # q streamed by the compaction pass itself
                 out = codec.compress_top_dense(g, k)
                 return out if on_device else out.cpu().numpy()
@@ -114,6 +127,14 @@ class Compression:
                     else np.zeros(0, dtype=np.float64))
         g = self._to_device(grad)
         codec_id = L.FC_CODEC_DROPOUT_BIASED if fn == 'dropout-biased' else L.FC_CODEC_DROPOUT_UNBIASED
+        if g.dtype == torch.float64:           # g * mask (/ p) in float64, exactly
+            if host_mask is not None:
+                mask = torch.from_numpy(bitmask_words(host_mask, n, True).view(np.int32)).to(g.device)
+                out = codec.mask_dense_f64(g, codec_id, p=float(p), mask_bits=mask)
+            else:
+                out = codec.mask_dense_f64(g, codec_id, p=float(p), seed=self.seed,
+                                           offset=self._next_offset())
+            return out if on_device else out.cpu().numpy()
         if host_mask is not None:
             mask = torch.from_numpy(bitmask_words(host_mask, n, True).view(np.int32)).to(g.device)
             pkt = codec.encode_mask(g, codec_id, p=float(p), mask_bits=mask)
@@ -146,12 +167,14 @@ class Compression:
         if isinstance(grad, torch.Tensor):
             if grad.dim() != 1:
                 raise ValueError("compress expects a 1-D gradient (client.py:53 flat vector)")
+            if grad.dtype not in (torch.float32, torch.float64):
+                raise TypeError(f"HIP codec handles float32/float64 gradients (got {grad.dtype})")
             return grad.contiguous()
         a = np.asarray(grad)
         if a.ndim != 1:
             raise ValueError("compress expects a 1-D gradient (client.py:53 flat vector)")
-        if a.dtype != np.float32:
-            raise TypeError(f"HIP codec handles float32 gradients (got {a.dtype}); "
+        if a.dtype not in (np.float32, np.float64):
+            raise TypeError(f"HIP codec handles float32/float64 gradients (got {a.dtype}); "
                             "see DESIGN.md §Scope")
         dev = torch.device(self.device) if self.device else torch.device("cuda")
         return torch.from_numpy(np.ascontiguousarray(a)).to(dev)

@@ -47,8 +47,7 @@ static WsPtrs ws_ptrs(void* ws, uint64_t n) {
   WsPtrs W;
   W.st = reinterpret_cast<TopkState*>(b);
   W.hist1 = reinterpret_cast<uint32_t*>(b + L.off_hist1);
-  W.hist2h = reinterpret_cast<uint32_t*>(b + L.off_hist2h);
-  W.hist2l = reinterpret_cast<uint32_t*>(b + L.off_hist2l);
+  W.tick = reinterpret_cast<uint32_t*>(b + L.off_tick);
   W.ehist = reinterpret_cast<uint32_t*>(b + L.off_ehist);
   W.chist = reinterpret_cast<uint32_t*>(b + L.off_chist);
   W.small = reinterpret_cast<uint64_t*>(b + L.off_small);
@@ -99,6 +98,25 @@ static SamplePlan make_plan(uint64_t n, uint64_t k) {
     if (P.r_lo > (int64_t)S) P.lo_all = 1;
   }
   if (P.r_hi < 1) P.hi_none = 1;
+  // pilot (k_sample1): kPilotSegs segments spread over the sample, read by every workgroup.
+  // Its ranks bracket the sample ranks scaled to the pilot, widened by 7 pilot sigmas + 8.
+  P.pstride = (P.nseg + kSampleSegs - 1) / kSampleSegs;          // the sample grid
+  P.np = 0;
+  while (P.np < (uint32_t)kPilotSegs && P.np * P.pstride < P.nseg) ++P.np;
+  double Sp = 0.0;
+  for (uint32_t j = 0; j < P.np; ++j) {
+    const uint64_t st = seg_start(P, pilot_seg(P, j));
+    const uint64_t lim = P.full ? std::min<uint64_t>(st + 1024, n) : st + 1024;
+    Sp += (double)(lim - st);
+  }
+  const double S = P.full ? (double)n : (double)P.nseg * 1024.0;
+  const double q = (double)k / (double)n;
+  const double sig = sqrt(Sp * q * (1.0 - q));
+  const int64_t isp = (int64_t)Sp;
+  P.pr_hi = std::max<int64_t>(1, (int64_t)floor((double)P.r_hi * Sp / S - 7.0 * sig - 8.0));
+  P.pr_lo = std::min<int64_t>(isp, (int64_t)ceil((double)P.r_lo * Sp / S + 7.0 * sig + 8.0));
+  if (P.pr_hi > isp) P.pr_hi = isp;
+  if (P.pr_lo < P.pr_hi) P.pr_lo = P.pr_hi;
   return P;
 }
 
@@ -138,6 +156,20 @@ struct TimedLaunch {
   ~TimedLaunch() { if (slot >= 0) (void)hipEventRecord(g_ev[slot].b, s); }
 };
 }  // namespace
+
+// k_sample1 for one client (jobs == nullptr) or a batch (grid.y = clients).
+static int launch_sample(int key_mode, dim3 grid, const float* g, const SamplePlan& P,
+                         uint64_t seed, uint64_t offset, const WsPtrs& W, uint32_t ib,
+                         fc_packet_hdr* hdr, const HdrInit& hi, const fc_encode_job* jobs,
+                         uint64_t stride, hipStream_t s) {
+  TimedLaunch t(FC_TIME_SAMPLE, s);
+  if (key_mode == FC_KEY_PHILOX)
+    hipLaunchKernelGGL(k_sample1<kKeyPhilox>, grid, dim3(kBlock), 0, s, g, P, seed, offset, W, ib, hdr, hi, jobs, stride);
+  else
+    hipLaunchKernelGGL(k_sample1<kKeyMag>, grid, dim3(kBlock), 0, s, g, P, seed, offset, W, ib, hdr, hi, jobs, stride);
+  FC_LAUNCHED("k_sample1");
+  return FC_OK;
+}
 
 static int launch_engine(int key_mode, const EngineArgs& base, int passes, hipStream_t s) {
   if (const char* dbg = getenv("FC_DEBUG_ENGINE_PASSES")) passes = atoi(dbg);  // debugging only
@@ -179,6 +211,14 @@ static int launch_resolve(const ResolveArgs& a, hipStream_t s) {
 extern "C" {
 
 int fc_abi_version(void) { return FC_ABI_VERSION; }
+#ifdef FC_TRACE
+// diagnostic builds only: copy the phase timestamps (fc_common.h FC_TR) to the host
+int fc_trace_read(uint64_t* host, size_t count) {
+  if (count > (1u << 16)) count = 1u << 16;
+  hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fc_trace), count * 8, 0, hipMemcpyDeviceToHost);
+  return e == hipSuccess ? FC_OK : fail(FC_ERR_HIP, "trace read: %s", hipGetErrorString(e));
+}
+#endif
 const char* fc_last_error(void) { return g_err; }
 uint64_t fc_num_chunks(uint64_t n) { return num_chunks(n); }
 size_t fc_workspace_bytes(uint64_t n) { return (size_t)WsLayout::of(n).bytes; }
@@ -276,20 +316,8 @@ int fc_topk_encode(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_
   hipStream_t s = (hipStream_t)stream;
   const SamplePlan P = make_plan(n, k);
   const uint32_t sgrid = (P.nseg + kSampleSegs - 1) / kSampleSegs;   // <= 256
-  {
-    TimedLaunch t(FC_TIME_SAMPLE, s);
-    if (key_mode == FC_KEY_PHILOX) {
-      hipLaunchKernelGGL((k_sample<kKeyPhilox, 1>), dim3(sgrid), dim3(kBlock), 0, s, g, P, seed, offset, ca.W, ca.ib, hdr, hi, nullptr, 0ull);
-      FC_LAUNCHED("k_sample1");
-      hipLaunchKernelGGL((k_sample<kKeyPhilox, 2>), dim3(sgrid), dim3(kBlock), 0, s, g, P, seed, offset, ca.W, ca.ib, hdr, hi, nullptr, 0ull);
-      FC_LAUNCHED("k_sample2");
-    } else {
-      hipLaunchKernelGGL((k_sample<kKeyMag, 1>), dim3(sgrid), dim3(kBlock), 0, s, g, P, seed, offset, ca.W, ca.ib, hdr, hi, nullptr, 0ull);
-      FC_LAUNCHED("k_sample1");
-      hipLaunchKernelGGL((k_sample<kKeyMag, 2>), dim3(sgrid), dim3(kBlock), 0, s, g, P, seed, offset, ca.W, ca.ib, hdr, hi, nullptr, 0ull);
-      FC_LAUNCHED("k_sample2");
-    }
-  }
+  rc = launch_sample(key_mode, dim3(sgrid), g, P, seed, offset, ca.W, ca.ib, hdr, hi, nullptr, 0ull, s);
+  if (rc) return rc;
   rc = launch_compact_key(key_mode, ca, s);
   if (rc) return rc;
   return launch_resolve(ra, s);
@@ -309,30 +337,16 @@ int fc_topk_encode_dense(const float* g, uint64_t n, uint64_t k, uint32_t* idx, 
   hipStream_t s = (hipStream_t)stream;
   const SamplePlan P = make_plan(n, k);
   const uint32_t sgrid = (P.nseg + kSampleSegs - 1) / kSampleSegs;
-  {
-    TimedLaunch t(FC_TIME_SAMPLE, s);
-    hipLaunchKernelGGL((k_sample<kKeyMag, 1>), dim3(sgrid), dim3(kBlock), 0, s, g, P, 0ull, 0ull, ca.W, ca.ib, hdr, hi, nullptr, 0ull);
-    FC_LAUNCHED("k_sample1");
-    hipLaunchKernelGGL((k_sample<kKeyMag, 2>), dim3(sgrid), dim3(kBlock), 0, s, g, P, 0ull, 0ull, ca.W, ca.ib, hdr, hi, nullptr, 0ull);
-    FC_LAUNCHED("k_sample2");
-  }
+  rc = launch_sample(FC_KEY_MAGNITUDE, dim3(sgrid), g, P, 0ull, 0ull, ca.W, ca.ib, hdr, hi, nullptr, 0ull, s);
+  if (rc) return rc;
   {
     TimedLaunch t(FC_TIME_COMPACT, s);
     hipLaunchKernelGGL(k_compact_mag1_dense, dim3(ca.nchunks, 1), dim3(kCBlock), 0, s, ca);
     FC_LAUNCHED("k_compact_mag1_dense");
   }
-  rc = launch_resolve(ra, s);
-  if (rc) return rc;
-  DenseFixArgs fa;
-  fa.hdr = hdr; fa.idx = idx; fa.val = val; fa.cnt = cnt; fa.ccnt = ca.W.ccnt; fa.cand = ca.W.cand;
-  fa.dense = dense; fa.ib = ca.ib; fa.nchunks = ca.nchunks;
-  {
-    TimedLaunch t(FC_TIME_DECODE, s);
-    const uint32_t grid = ca.nchunks < 1024u ? ca.nchunks : 1024u;
-    hipLaunchKernelGGL(k_dense_fixup, dim3(grid), dim3(kBlock), 0, s, fa);
-    FC_LAUNCHED("k_dense_fixup");
-  }
-  return FC_OK;
+  // k_resolve publishes T64 to its own workgroups, which then zero the slack in q
+  ra.dense = dense;
+  return launch_resolve(ra, s);
 }
 
 size_t fc_workspace_bytes_batch(uint64_t n, int m) {
@@ -372,20 +386,8 @@ int fc_topk_encode_batch(const fc_encode_job* jobs, int m, uint64_t n, uint64_t 
   hipStream_t s = (hipStream_t)stream;
   const SamplePlan P = make_plan(n, k);
   const dim3 sgrid((P.nseg + kSampleSegs - 1) / kSampleSegs, (uint32_t)m);
-  {
-    TimedLaunch t(FC_TIME_SAMPLE, s);
-    if (key_mode == FC_KEY_PHILOX) {
-      hipLaunchKernelGGL((k_sample<kKeyPhilox, 1>), sgrid, dim3(kBlock), 0, s, nullptr, P, 0ull, 0ull, ca.W, ib, nullptr, hi, jobs, stride);
-      FC_LAUNCHED("k_sample1(batch)");
-      hipLaunchKernelGGL((k_sample<kKeyPhilox, 2>), sgrid, dim3(kBlock), 0, s, nullptr, P, 0ull, 0ull, ca.W, ib, nullptr, hi, jobs, stride);
-      FC_LAUNCHED("k_sample2(batch)");
-    } else {
-      hipLaunchKernelGGL((k_sample<kKeyMag, 1>), sgrid, dim3(kBlock), 0, s, nullptr, P, 0ull, 0ull, ca.W, ib, nullptr, hi, jobs, stride);
-      FC_LAUNCHED("k_sample1(batch)");
-      hipLaunchKernelGGL((k_sample<kKeyMag, 2>), sgrid, dim3(kBlock), 0, s, nullptr, P, 0ull, 0ull, ca.W, ib, nullptr, hi, jobs, stride);
-      FC_LAUNCHED("k_sample2(batch)");
-    }
-  }
+  int rc = launch_sample(key_mode, sgrid, nullptr, P, 0ull, 0ull, ca.W, ib, nullptr, hi, jobs, stride, s);
+  if (rc) return rc;
   {
     TimedLaunch t(FC_TIME_COMPACT, s);
     const dim3 grid(ca.nchunks, (uint32_t)m);
@@ -628,6 +630,88 @@ int fc_weighted_sum_dense(const float* const* rows, const float* w, int m, uint6
   hipLaunchKernelGGL(k_wsum, dim3((uint32_t)blocks), dim3(kBlock), 0, (hipStream_t)stream, rows,
                      w, m, n, out);
   FC_LAUNCHED("k_wsum");
+  return FC_OK;
+}
+
+// ---- float64 gradients (attack_models.py:105-106 -> aggregation.py:61) -------------------
+static uint32_t grid_of(uint64_t n) {
+  uint64_t b = (n + kBlock - 1) / kBlock;
+  if (b < 1) b = 1;
+  if (b > 2048) b = 2048;
+  return (uint32_t)b;
+}
+
+int fc_topk_dense_f64(const double* g, uint64_t n, uint64_t k, int key_mode, uint64_t seed,
+                      uint64_t offset, double* out, void* ws, size_t ws_bytes,
+                      fc_stream_t stream) {
+  FC_CHECK(g && out && ws, "NULL argument");
+  FC_CHECK(n >= 1 && n <= 0xffffffffull, "n=%llu outside [1, 2^32-1]", (unsigned long long)n);
+  FC_CHECK(k <= n, "k=%llu > n=%llu (pass the effective k)", (unsigned long long)k,
+           (unsigned long long)n);
+  FC_CHECK(key_mode == FC_KEY_MAGNITUDE || key_mode == FC_KEY_PHILOX, "bad key_mode %d", key_mode);
+  if (ws_bytes < WsLayout::of(n).bytes)
+    return fail(FC_ERR_WORKSPACE, "workspace %zu B < %llu B needed", ws_bytes,
+                (unsigned long long)WsLayout::of(n).bytes);
+  const WsPtrs W = ws_ptrs(ws, n);
+  Engine64Args a;
+  memset(&a, 0, sizeof a);
+  a.g = g; a.n = n; a.k = k; a.seed = seed; a.offset = offset; a.key_mode = (uint32_t)key_mode;
+  a.E = reinterpret_cast<Eng64State*>(static_cast<char*>(ws) + kEng64Off);
+  a.hist = W.ehist;
+  a.small = reinterpret_cast<u128*>(W.small);
+  hipStream_t s = (hipStream_t)stream;
+  for (int p = 0; p < 8; ++p) {                  // 95-bit comps, 12-bit digits: <= 8 passes
+    TimedLaunch t(FC_TIME_ENGINE, s);
+    a.first = p == 0;
+    if (key_mode == FC_KEY_PHILOX) hipLaunchKernelGGL(k_engine64<kKeyPhilox>, dim3(kEngineGrid), dim3(kBlock), 0, s, a);
+    else hipLaunchKernelGGL(k_engine64<kKeyMag>, dim3(kEngineGrid), dim3(kBlock), 0, s, a);
+    FC_LAUNCHED("k_engine64");
+  }
+  TimedLaunch t(FC_TIME_COMPACT, s);
+  if (key_mode == FC_KEY_PHILOX)
+    hipLaunchKernelGGL(k_select_dense64<kKeyPhilox>, dim3(grid_of(n)), dim3(kBlock), 0, s, g, n, k, seed, offset, a.E, out);
+  else
+    hipLaunchKernelGGL(k_select_dense64<kKeyMag>, dim3(grid_of(n)), dim3(kBlock), 0, s, g, n, k, seed, offset, a.E, out);
+  FC_LAUNCHED("k_select_dense64");
+  return FC_OK;
+}
+
+int fc_mask_dense_f64(const double* g, uint64_t n, int codec, const uint32_t* mask_bits, double p,
+                      uint64_t seed, uint64_t offset, double* out, fc_stream_t stream) {
+  FC_CHECK(g && out, "NULL argument");
+  FC_CHECK(n >= 1 && n <= 0xffffffffull, "n=%llu outside [1, 2^32-1]", (unsigned long long)n);
+  FC_CHECK(codec == FC_CODEC_DROPOUT_BIASED || codec == FC_CODEC_DROPOUT_UNBIASED ||
+               codec == FC_CODEC_RAND, "bad codec %d", codec);
+  FC_CHECK(mask_bits || codec != FC_CODEC_RAND, "native rand-k uses fc_topk_dense_f64(PHILOX)");
+  FC_CHECK(mask_bits || (p >= 0.0 && p <= 1.0), "p=%g outside [0, 1]", p);
+  double thr = floor(p * 4294967296.0 + 0.5);
+  if (thr < 0) thr = 0;
+  if (thr > 4294967296.0) thr = 4294967296.0;
+  const int mode = codec == FC_CODEC_RAND ? 0 : codec == FC_CODEC_DROPOUT_BIASED ? 1 : 2;
+  hipStream_t s = (hipStream_t)stream;
+  TimedLaunch t(FC_TIME_COMPACT, s);
+  hipLaunchKernelGGL(k_mask_dense64, dim3(grid_of(n)), dim3(kBlock), 0, s, g, n, mask_bits,
+                     (uint64_t)thr, seed, offset, mode, p, out);
+  FC_LAUNCHED("k_mask_dense64");
+  return FC_OK;
+}
+
+int fc_weighted_sum_dense_f64(const void* const* rows, int rows_f64, const double* w, int m,
+                              uint64_t n, double* out, int continue_sum, fc_stream_t stream) {
+  FC_CHECK(rows && w && out, "NULL argument");
+  FC_CHECK(m >= 1, "m=%d < 1", m);
+  FC_CHECK(n >= 1, "n=0");
+  hipLaunchKernelGGL(k_wsum64, dim3(grid_of(n)), dim3(kBlock), 0, (hipStream_t)stream, rows,
+                     rows_f64, w, m, n, out, continue_sum);
+  FC_LAUNCHED("k_wsum64");
+  return FC_OK;
+}
+
+int fc_div_scalar_f64(double* x, uint64_t n, double d, fc_stream_t stream) {
+  FC_CHECK(x != nullptr, "x is NULL");
+  FC_CHECK(n >= 1, "n=0");
+  hipLaunchKernelGGL(k_div_scalar64, dim3(grid_of(n)), dim3(kBlock), 0, (hipStream_t)stream, x, n, d);
+  FC_LAUNCHED("k_div_scalar64");
   return FC_OK;
 }
 

@@ -128,6 +128,17 @@ __device__ __forceinline__ float4 load4(const float* __restrict__ g, uint64_t e,
   if (e + 3 < n) r.w = g[e + 3];
   return r;
 }
+// float4 load of [e, e+4) with zero fill past n, default cache policy (latency-bound reads:
+// the sample, where non-temporal loads measured ~2 us slower)
+__device__ __forceinline__ float4 load4_plain(const float* __restrict__ g, uint64_t e, uint64_t n) {
+  if (e + 4 <= n) return *reinterpret_cast<const float4*>(g + e);
+  float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (e + 0 < n) r.x = g[e + 0];
+  if (e + 1 < n) r.y = g[e + 1];
+  if (e + 2 < n) r.z = g[e + 2];
+  if (e + 3 < n) r.w = g[e + 3];
+  return r;
+}
 // Unconditional float4 load through the GLOBAL address space.  Pointers that come out of
 // memory (batched job tables) are generic to the compiler, and a generic load is a flat_load
 // that also counts in lgkmcnt; a per-element bounds branch between loads made hipcc wait for
@@ -147,6 +158,20 @@ __device__ __forceinline__ float f4get(const float4& v, int j) {
 }
 __device__ __forceinline__ void f4set(float4& v, int j, float x) {
   if (j == 0) v.x = x; else if (j == 1) v.y = x; else if (j == 2) v.z = x; else v.w = x;
+}
+
+// h[0..4096) = gh[0..4096) (sc1 loads), then gh = 0 — every load issued before any clearing
+// store (a load and a store of one address issue in order: interleaved, each bin cost a round
+// trip).  256-thread workgroup; the caller synchronises before reading h.
+__device__ __forceinline__ void load_clear_hist(uint32_t* gh, uint32_t* h) {
+  constexpr int kPer = 4096 / 256;
+  uint32_t v[kPer];
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) v[j] = ld_agent(&gh[j * 256 + threadIdx.x]);
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) h[j * 256 + threadIdx.x] = v[j];
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) st_agent(&gh[j * 256 + threadIdx.x], 0u);
 }
 
 // Spread the 8 bits of x to bits 0,4,8,...,28 (bitmap assembly from 4 ballots).
@@ -182,15 +207,61 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_tmp,
   return base + inc - v;
 }
 
+// ---- diagnostic phase timestamps (FC_TRACE builds only; tools/trace_probe.py) ----------
+// FC_TR(slot): thread 0 of the workgroup records s_memrealtime (100 MHz) at trace[block*32+slot].
+#ifdef FC_TRACE
+__device__ uint64_t g_fc_trace[1 << 16];
+#define FC_TR(slot)                                                                          \
+  do {                                                                                      \
+    if (threadIdx.x == 0)                                                                   \
+      g_fc_trace[((blockIdx.x + blockIdx.y * gridDim.x) * 32u + (slot)) & 0xffffu] =        \
+          __builtin_amdgcn_s_memrealtime();                                                 \
+  } while (0)
+#else
+#define FC_TR(slot) do {} while (0)
+#endif
+
 // Last-arriver ticket for payloads written ONLY by agent-scope atomics or sc1 stores and
 // read ONLY by sc1 loads / atomics (MI355X_MICROARCH.md §visibility, "Hand-offs measured
 // with sc1 loads": every storing wave drains, barrier, one lane adds; the workgroup whose
 // add returned nblocks-1 loads after a barrier).  No L2 write-back fence needed.
 __device__ __forceinline__ bool last_block_arrive_sc1(uint32_t* counter, uint32_t nblocks,
-                                                      uint32_t* s_flag) {
+                                                      uint32_t* s_flag, int tr = -1) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if (tr >= 0) FC_TR(tr);
   if (threadIdx.x == 0) *s_flag = (atomicAdd(counter, 1u) == nblocks - 1) ? 1u : 0u;
+  if (tr >= 0) FC_TR(tr + 1);
+  __syncthreads();
+  return *s_flag != 0;
+}
+
+// Two-level last-arriver ticket over nblocks workgroups (bid = this workgroup's index among
+// them): the workgroups count into G <= 16 group counters on separate 256-B lines, the last of
+// each group into one top counter.  Same-address atomics queue at ~35 ns each (256 workgroups
+// on ONE counter took ~9 us, FC_TRACE); this keeps every queue at <= 16.  Payload rules are
+// those of last_block_arrive_sc1 (sc1 stores drained before the first add; sc1 loads after).
+// Each group's last arriver and the top's reset their counters: self-cleaning.
+__device__ __forceinline__ bool last_block_arrive_tree(uint32_t* tick, uint32_t nblocks,
+                                                       uint32_t bid, uint32_t* s_flag,
+                                                       int tr = -1) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tr >= 0) FC_TR(tr);
+  if (threadIdx.x == 0) {
+    constexpr uint32_t kG = 16, kS = 64;             // fc_state.h kTickGroups / kTickStride
+    const uint32_t G = nblocks < kG ? nblocks : kG;
+    const uint32_t g = bid % G;
+    const uint32_t gsize = nblocks / G + (g < nblocks % G ? 1u : 0u);
+    bool last = false;
+    if (atomicAdd(&tick[g * kS], 1u) == gsize - 1) {
+      st_agent(&tick[g * kS], 0u);
+      last = atomicAdd(&tick[kG * kS], 1u) == G - 1;
+      if (last) st_agent(&tick[kG * kS], 0u);
+    }
+    *s_flag = last ? 1u : 0u;
+  }
+  if (tr >= 0) FC_TR(tr + 1);
   __syncthreads();
   return *s_flag != 0;
 }

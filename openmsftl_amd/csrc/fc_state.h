@@ -16,32 +16,38 @@ struct alignas(16) TopkState {
   uint64_t e_prefix;     // exact radix engine: resolved high bits of T64
   uint32_t err;          // sticky device error (spin timeout)
   uint32_t a_done, b_done, r_done;
-  uint32_t b1_hi, b1_lo; // level-1 sample bins of the two bracket ranks
-  uint32_t rr_hi, rr_lo; // residual 1-based ranks inside those bins
-  uint32_t hi_none, lo_all;
+  uint32_t win_klo, win_khi, win_fs;   // k_sample1's fine window, published by workgroup 0
+  uint32_t win_flag;     // 1 once the window is published; reset by the sample's last block
+  uint32_t pad1_[2];
   uint32_t t_lo, t_hi;   // bracket (keys): list key >= t_lo; candidates key <= t_hi
   uint32_t sbin;         // candidate histogram bin = (key - t_lo) >> sbin  (< 4096 bins)
   uint32_t cand_on, n_cand, cand_over, ent_over;
   uint32_t small_n;      // survivors gathered for the LDS finish
   uint32_t e_shift, e_rank, e_matched, e_done, e_ticket, e_status;
-  uint32_t pad_[6];
+  uint32_t gen;          // k_resolve generation: bumped when T64 is published (dense fix-up)
+  uint32_t st_pub;       // status published with T_pub
+  uint64_t T_pub;        // T64 published to the waiting k_resolve workgroups
+  uint32_t pad_[2];
   uint32_t shard_ent[kShards];   // k_compact totals, 64-way sharded (no hot word)
   uint32_t shard_cnd[kShards];
 };
 static_assert(sizeof(TopkState) <= 1024, "state block");
 
+constexpr int kSampleShards = 8;            // k_sample1's global histogram, sharded by workgroup
+constexpr int kTickGroups = 16;             // two-level last-arriver tickets (fc_common.h)
+constexpr int kTickStride = 64;             // u32 per ticket counter (one 256-B line each)
+constexpr int kTickWords = (kTickGroups + 1) * kTickStride;
+
 struct WsLayout {
   uint64_t nchunks, cand_cap;
-  uint64_t off_hist1, off_hist2h, off_hist2l, off_ehist, off_chist, off_small, off_status,
-      off_cand, bytes;
+  uint64_t off_hist1, off_tick, off_ehist, off_chist, off_small, off_status, off_cand, bytes;
   __host__ __device__ static WsLayout of(uint64_t n) {
     WsLayout L;
     L.nchunks = (n + kChunk - 1) / kChunk;
     L.cand_cap = L.nchunks * kCandSlot;                // per-chunk candidate slots
     uint64_t o = 1024;
-    L.off_hist1 = o;  o += 4ull * kHistBins;
-    L.off_hist2h = o; o += 4ull * kHistBins;
-    L.off_hist2l = o; o += 4ull * kHistBins;
+    L.off_hist1 = o;  o += 4ull * kHistBins * kSampleShards;
+    L.off_tick = o;   o += 4ull * kTickWords * 2;      // sample ticket, resolve ticket
     L.off_ehist = o;  o += 4ull * kHistBins;
     L.off_chist = o;  o += 4ull * kHistBins;
     L.off_small = o;  o += 8ull * kSmallCap;
@@ -61,7 +67,7 @@ struct HdrInit {          // static header fields, written by the first kernel o
 
 struct WsPtrs {
   TopkState* st;
-  uint32_t *hist1, *hist2h, *hist2l, *ehist, *chist;
+  uint32_t *hist1, *tick, *ehist, *chist;   // hist1: kSampleShards x 4096; tick: 2 tickets
   uint64_t* small;
   uint32_t* ccnt;          // candidates per chunk (may exceed kCandSlot: overflowed chunk)
   uint64_t* cand;          // chunk c's candidates at [c * kCandSlot, + min(ccnt, kCandSlot))
@@ -72,8 +78,7 @@ struct WsPtrs {
 __device__ __forceinline__ WsPtrs ws_shift(WsPtrs W, uint64_t bytes) {
   W.st = reinterpret_cast<TopkState*>(reinterpret_cast<char*>(W.st) + bytes);
   W.hist1 = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(W.hist1) + bytes);
-  W.hist2h = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(W.hist2h) + bytes);
-  W.hist2l = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(W.hist2l) + bytes);
+  W.tick = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(W.tick) + bytes);
   W.ehist = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(W.ehist) + bytes);
   W.chist = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(W.chist) + bytes);
   W.small = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(W.small) + bytes);
@@ -98,12 +103,21 @@ struct SamplePlan {
   uint32_t full;       // 1: segments tile [0, n) exactly (n <= kFullSampleMax)
   int64_t r_hi, r_lo;  // 1-based ranks from the top inside the sample
   uint32_t hi_none, lo_all;
+  uint32_t np;         // pilot segments (<= kPilotSegs): workgroup 0's own segments
+  uint32_t pstride;    // their spacing = the sample grid (segment j*pstride, j < np)
+  int64_t pr_hi, pr_lo;  // pilot ranks (1-based from the top) that bound the fine window
 };
+constexpr int kPilotSegs = 4;                 // = kSampleSegs: the pilot IS workgroup 0's share
 constexpr uint64_t kFullSampleMax = 1ull << 20;
 
-__device__ __forceinline__ uint64_t seg_start(const SamplePlan& P, uint32_t s) {
+__host__ __device__ __forceinline__ uint64_t seg_start(const SamplePlan& P, uint32_t s) {
   if (P.full || P.nseg == 1) return (uint64_t)s * 1024;
   return ((uint64_t)s * (P.n - 1024) / (P.nseg - 1)) & ~3ull;
+}
+// pilot segment j (< P.np): workgroup 0's segment j (spread over the gradient: the sample's
+// segments are stratified and workgroup 0 takes every pstride-th one)
+__host__ __device__ __forceinline__ uint32_t pilot_seg(const SamplePlan& P, uint32_t j) {
+  return j * P.pstride;
 }
 
 }  // namespace fc

@@ -1,19 +1,21 @@
 // fc_topk.hip — top-k / native rand-k encode for MI355X (gfx950).
 //
 // Replaces compression.py:31-45 (argsort(|g|)[::-1][:k] / permutation[:k]).  Fast path =
-// four launches, ONE streaming read of g:
+// three launches, ONE streaming read of g:
 //
-//   k_sample<1>, k_sample<2>  stratified sample (<= 1 M keys, < 1 % of g) -> two-level
-//                             4096-bin histograms -> key bracket [t_lo, t_hi] around the
-//                             k-th key (+-6 sigma of the sample quantile)
-//   k_compact                 one pass over g, one independent 256-thread workgroup per
-//                             8192-element chunk: every element with key >= t_lo is written
-//                             (idx, val) in ascending index order into the chunk's SLOT of the
-//                             packet ([c*8192, c*8192 + cnt[c])) — no global scan, no
-//                             look-back; keys inside the bracket ("candidates") also go to the
-//                             chunk's candidate slot and a 4096-bin histogram
+//   k_sample1                 stratified sample (<= 1 M keys, < 1 % of g) -> one 4096-bin
+//                             histogram whose fine window a pilot sub-sample places -> key
+//                             bracket [t_lo, t_hi] around the k-th key (+-6 sigma of the
+//                             sample quantile)
+//   k_compact                 one pass over g, one independent workgroup per 8192-element
+//                             chunk: every element with key >= t_lo is written (idx, val) in
+//                             ascending index order into the chunk's SLOT of the packet
+//                             ([c*8192, c*8192 + cnt[c])) — no global scan, no look-back; keys
+//                             inside the bracket ("candidates") also go to the chunk's
+//                             candidate slot and a 4096-bin histogram
 //   k_resolve                 histogram -> the bin holding rank r = k - #(key > t_hi);
 //                             gather that bin's candidates; LDS bitonic sort -> exact T64
+//                             (dense output: the same launch then zeroes the slack in q)
 //
 // Anything unusual (bracket missed, candidate list overflow, > 4096 survivors) sets
 // FC_STATUS_RETRY_EXACT; fc_topk_encode_exact then runs k_engine (12-bit radix select over
@@ -69,6 +71,34 @@ __device__ void find_rank_desc(const uint32_t* h, uint32_t rank1, uint32_t* s_tm
   __syncthreads();
 }
 
+// Both ranks of find_rank_desc in one scan: s_out[0..1] for r1, s_out[2..3] for r2 (bin 0,
+// rank 1 when a rank is outside [1, total]).  256-thread workgroup; 2 barriers + 1.
+__device__ void find_ranks_desc(const uint32_t* h, uint32_t r1, uint32_t r2, uint32_t* s_tmp,
+                                uint32_t* s_out) {
+  const int t = threadIdx.x;
+  constexpr int per = kHistBins / kBlock;
+  const int top = kHistBins - 1 - per * t;
+  uint32_t hv[per], sum = 0;
+#pragma unroll
+  for (int b = 0; b < per; ++b) { hv[b] = h[top - b]; sum += hv[b]; }
+  uint32_t total;
+  const uint32_t excl = block_excl_scan(sum, s_tmp, &total);
+  auto find = [&](uint32_t r, int o) {
+    if (r > excl && r <= excl + sum) {
+      uint32_t c = excl;
+#pragma unroll
+      for (int b = 0; b < per; ++b) {
+        if (r > c && r <= c + hv[b]) { s_out[o] = (uint32_t)(top - b); s_out[o + 1] = r - c; }
+        c += hv[b];
+      }
+    }
+    if (t == 0 && !(r >= 1 && r <= total)) { s_out[o] = 0; s_out[o + 1] = 1; }
+  };
+  find(r1, 0);
+  find(r2, 2);
+  __syncthreads();
+}
+
 // Descending bitonic sort of P2 (power of two) uint64 values in LDS (256 threads).
 __device__ void bitonic_desc(uint64_t* sv, uint32_t P2) {
   for (uint32_t size = 2; size <= P2; size <<= 1) {
@@ -85,27 +115,128 @@ __device__ void bitonic_desc(uint64_t* sv, uint32_t P2) {
 }
 
 // --------------------------------------------------------------------------------------
-// Sampling: level 1 (key >> 19, 4096 bins) and level 2 ((key >> 7) & 0xfff inside the two
-// level-1 bins that hold the bracket ranks).  Payload = global atomics only.
+// k_sample1: the bracket [t_lo, t_hi] around the k-th key in ONE launch.
+//
+// Every workgroup first reads the same small PILOT (kPilotSegs sample segments, <= 8 K keys,
+// L2-resident after the first reader) and finds, in an LDS histogram of key >> 19, the
+// level-1 bins holding the pilot ranks pr_hi / pr_lo (the sample bracket ranks scaled to the
+// pilot, widened by 7 pilot sigmas).  That fixes the same key window [klo, khi] in every
+// workgroup, so their histograms of the real sample (<= 1 M keys, 4 segments per workgroup)
+// can share one 4096-bin layout without a second launch:
+//   bins    0..1023  coarse, key >> 21, keys below the window
+//   bins 1024..3071  fine, (key - klo) >> fs, the window (>= 256 key units per bin)
+//   bins 3072..4095  coarse, key >> 21, keys above the window
+// Bin order is key order, so the last workgroup reads the bracket ranks straight off the
+// summed histogram.  A pilot that misjudges the window only coarsens the bracket (more
+// candidates), it cannot make it wrong.  (Two launches — level 1 on key >> 19, level 2 on
+// (key >> 7) & 0xfff — took 17.8 + 21.5 us per 128 M gradient.)
 // --------------------------------------------------------------------------------------
 #ifndef FC_SAMPLE_SEGS_PER_WG
 #define FC_SAMPLE_SEGS_PER_WG 4
 #endif
-// segments per workgroup (grid = ceil(nseg / 4)).  Measured per 128 M client (two launches):
-// 1 / 2 / 4 / 8 / 16 per WG = 65 / 50 / 45 / 47 / 60 us (more WGs: more histogram flush atomics;
-// fewer: less latency hiding).
 constexpr int kSampleSegs = FC_SAMPLE_SEGS_PER_WG;
+constexpr uint32_t kSpinMax = 1u << 18;   // bounded spins (~60 ms): one that never ends is a bug
+constexpr uint32_t kFineLo = 1024, kFineBins = 2048, kFineHi = kFineLo + kFineBins;
+constexpr uint32_t kCoarseShift = 21;            // 0x7fffffff >> 21 = 1023
 
-template <int KM, int LEVEL>
-__global__ __launch_bounds__(kBlock) void k_sample(const float* __restrict__ g, SamplePlan P,
-                                                   uint64_t seed, uint64_t off, WsPtrs W,
-                                                   uint32_t ib, fc_packet_hdr* hdr,
-                                                   HdrInit HI, const fc_encode_job* jobs,
-                                                   uint64_t ws_stride) {
-  __shared__ uint32_t ha[kHistBins];
-  __shared__ uint32_t hb[LEVEL == 2 ? kHistBins : 1];
-  __shared__ uint32_t s_tmp[8], s_out[4], s_flag;
-  if (jobs) {                                   // batched: client blockIdx.y
+struct FineWin {
+  uint32_t klo, khi, fs;
+};
+__device__ __forceinline__ uint32_t fine_bin(uint32_t key, const FineWin& F) {
+  if (key > F.khi) return kFineHi + (key >> kCoarseShift);
+  if (key >= F.klo) return kFineLo + ((key - F.klo) >> F.fs);
+  return key >> kCoarseShift;
+}
+__device__ __forceinline__ uint32_t fine_lower(uint32_t b, const FineWin& F) {
+  if (b >= kFineHi) return max(F.khi + 1u, (b - kFineHi) << kCoarseShift);
+  if (b >= kFineLo) return F.klo + ((b - kFineLo) << F.fs);
+  return b << kCoarseShift;
+}
+__device__ __forceinline__ uint32_t fine_upper(uint32_t b, const FineWin& F) {
+  uint64_t u;
+  if (b >= kFineHi) {
+    u = ((uint64_t)(b - kFineHi + 1) << kCoarseShift) - 1;
+  } else if (b >= kFineLo) {
+    u = (uint64_t)F.klo + ((uint64_t)(b - kFineLo + 1) << F.fs) - 1;
+    if (u > F.khi) u = F.khi;
+  } else {
+    u = ((uint64_t)(b + 1) << kCoarseShift) - 1;
+    if (u + 1 > F.klo) u = F.klo - 1ull;            // klo > 0 whenever a key lands below it
+  }
+  return u > 0xffffffffull ? 0xffffffffu : (uint32_t)u;
+}
+
+// Segment s of the sample: element range [e, lim) of this thread's float4.
+__device__ __forceinline__ void seg_lane(const SamplePlan& P, uint32_t s, int tid, uint64_t& e,
+                                         uint64_t& lim) {
+  const uint64_t st = seg_start(P, s);
+  lim = P.full ? (st + 1024 < P.n ? st + 1024 : P.n) : st + 1024;
+  e = st + (uint64_t)tid * 4;
+}
+
+// Pilot level-1 histogram (key >> 19) of the kPilotSegs pilot segments -> the window.
+// own: this workgroup IS workgroup 0 (its segments xs / es / ls are the pilot, already loaded).
+template <int KM>
+__device__ __forceinline__ FineWin pilot_window(const float* __restrict__ g, const SamplePlan& P,
+                                                uint64_t seed, uint64_t off, uint32_t* h,
+                                                uint32_t* s_tmp, uint32_t* s_out, bool own,
+                                                const float4 (&xs)[kSampleSegs],
+                                                const uint64_t (&es)[kSampleSegs],
+                                                const uint64_t (&ls)[kSampleSegs]) {
+  static_assert(kPilotSegs == kSampleSegs, "the pilot is workgroup 0's share of the sample");
+  const int tid = threadIdx.x;
+  float4 xp[kPilotSegs];
+  uint64_t ep[kPilotSegs], lp[kPilotSegs];
+#pragma unroll
+  for (int q = 0; q < kPilotSegs; ++q) {
+    if (own) {
+      xp[q] = xs[q]; ep[q] = es[q]; lp[q] = ls[q];
+      continue;
+    }
+    ep[q] = lp[q] = 0;
+    xp[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if ((uint32_t)q < P.np) {
+      seg_lane(P, pilot_seg(P, (uint32_t)q), tid, ep[q], lp[q]);
+      if (ep[q] < lp[q]) xp[q] = load4_plain(g, ep[q], lp[q]);
+    }
+  }
+  __syncthreads();                                  // h zeroed by the caller
+  FC_TR(20);
+#pragma unroll
+  for (int q = 0; q < kPilotSegs; ++q) {
+    if (ep[q] < lp[q]) {
+      const uint4 kk = keys4<KM>(xp[q], ep[q], seed, off);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (ep[q] + j < lp[q]) atomicAdd(&h[u4get(kk, j) >> 19], 1u);
+    }
+  }
+  __syncthreads();
+  FC_TR(21);
+  find_ranks_desc(h, (uint32_t)P.pr_hi, (uint32_t)P.pr_lo, s_tmp, s_out);
+  FC_TR(22);
+  FineWin F;
+  F.klo = s_out[2] << 19;
+  F.khi = ((s_out[0] + 1u) << 19) - 1u;
+  F.fs = 0;
+  while (((F.khi - F.klo) >> F.fs) >= kFineBins) ++F.fs;
+  return F;
+}
+
+// One launch: grid (ceil(nseg / kSampleSegs), clients).  A lone client's launch (<= 256
+// workgroups, always co-resident) has workgroup 0 compute the window and publish it (sc1
+// payload + flag; the others load their segments meanwhile): 256 workgroups re-reading the same
+// 32 KB pilot took ~7 us of loads.  A batched launch (too many workgroups to wait on each
+// other) has every workgroup compute the window itself.
+template <int KM>
+__global__ __launch_bounds__(kBlock) void k_sample1(const float* __restrict__ g, SamplePlan P,
+                                                    uint64_t seed, uint64_t off, WsPtrs W,
+                                                    uint32_t ib, fc_packet_hdr* hdr, HdrInit HI,
+                                                    const fc_encode_job* jobs,
+                                                    uint64_t ws_stride) {
+  __shared__ uint32_t h[kHistBins];               // pilot histogram, then the sample's
+  __shared__ uint32_t s_tmp[8], s_out[4], s_flag, s_win[3];
+  if (jobs) {                                     // batched: client blockIdx.y
     const fc_encode_job& J = jobs[blockIdx.y];
     g = J.g; hdr = J.hdr; seed = J.seed; off = J.offset;
     HI.seed = seed; HI.offset = off;
@@ -113,88 +244,103 @@ __global__ __launch_bounds__(kBlock) void k_sample(const float* __restrict__ g, 
   }
   TopkState* S = W.st;
   const int tid = threadIdx.x;
-  for (int b = tid; b < kHistBins; b += kBlock) { ha[b] = 0; if (LEVEL == 2) hb[b] = 0; }
-  if (LEVEL == 1 && blockIdx.x == 0 && tid == 0) write_hdr_static(hdr, HI);
-  uint32_t b1_hi = 0, b1_lo = 0, hi_none = 0, lo_all = 0;
-  if (LEVEL == 2) { b1_hi = S->b1_hi; b1_lo = S->b1_lo; hi_none = S->hi_none; lo_all = S->lo_all; }
-  __syncthreads();
-  // all of this workgroup's segments loaded up front (one memory latency, not kSampleSegs)
+  FC_TR(0);
+  // this workgroup's segments first (plain loads: ~2 us sooner than non-temporal here)
   float4 xs[kSampleSegs];
-  uint64_t es[kSampleSegs], lims[kSampleSegs];
+  uint64_t es[kSampleSegs], ls[kSampleSegs];
 #pragma unroll
   for (int q = 0; q < kSampleSegs; ++q) {
     const uint32_t s = blockIdx.x + (uint32_t)q * gridDim.x;
-    es[q] = lims[q] = 0;
+    es[q] = ls[q] = 0;
     xs[q] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (s < P.nseg) {
-      const uint64_t st = seg_start(P, s);
-      lims[q] = P.full ? (st + 1024 < P.n ? st + 1024 : P.n) : st + 1024;
-      es[q] = st + (uint64_t)tid * 4;
-      if (es[q] < lims[q]) xs[q] = load4(g, es[q], lims[q]);
+      seg_lane(P, s, tid, es[q], ls[q]);
+      if (es[q] < ls[q]) xs[q] = load4_plain(g, es[q], ls[q]);
     }
   }
+  for (int b = tid; b < kHistBins; b += kBlock) h[b] = 0;
+  if (blockIdx.x == 0 && tid == 0) write_hdr_static(hdr, HI);
+  const bool shared_pilot = gridDim.y == 1;       // uniform
+  FineWin F;
+  if (!shared_pilot || blockIdx.x == 0) {
+    F = pilot_window<KM>(g, P, seed, off, h, s_tmp, s_out, blockIdx.x == 0, xs, es, ls);
+    if (shared_pilot && tid == 0) {               // publish: sc1 payload, drained, sc1 flag
+      st_agent(&S->win_klo, F.klo); st_agent(&S->win_khi, F.khi); st_agent(&S->win_fs, F.fs);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      st_agent(&S->win_flag, 1u);
+    }
+    for (int b = tid; b < kHistBins; b += kBlock) h[b] = 0;   // find_ranks_desc ended on a barrier
+  } else {
+    if (tid == 0) {                               // relaxed sc1 poll (bounded), sc1 payload
+      uint32_t it = 0;
+      while (ld_agent(&S->win_flag) == 0u && ++it < kSpinMax) __builtin_amdgcn_s_sleep(2);
+      s_win[0] = ld_agent(&S->win_klo); s_win[1] = ld_agent(&S->win_khi);
+      s_win[2] = it < kSpinMax ? ld_agent(&S->win_fs) : 0xffu;   // timeout: poisoned
+    }
+    __syncthreads();
+    F.klo = s_win[0]; F.khi = s_win[1]; F.fs = s_win[2];
+    if (F.fs == 0xffu) {                          // never expected: make the resolve retry
+      if (tid == 0) st_agent(&S->err, 1u);
+      F.klo = 0; F.khi = 0xffffffffu; F.fs = 31;
+    }
+  }
+  __syncthreads();
+  FC_TR(2);
+  // ---- this workgroup's share of the sample ----
 #pragma unroll
   for (int q = 0; q < kSampleSegs; ++q) {
-    const uint64_t e = es[q], lim = lims[q];
-    if (e < lim) {
-      const uint4 kk = keys4<KM>(xs[q], e, seed, off);
+    if (es[q] < ls[q]) {
+      const uint4 kk = keys4<KM>(xs[q], es[q], seed, off);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (e + j >= lim) break;
-        const uint32_t key = u4get(kk, j);
-        if (LEVEL == 1) {
-          atomicAdd(&ha[key >> 19], 1u);
-        } else {
-          const uint32_t b1 = key >> 19, b2 = (key >> 7) & 0xfffu;
-          if (!hi_none && b1 == b1_hi) atomicAdd(&ha[b2], 1u);
-          if (!lo_all && b1 == b1_lo) atomicAdd(&hb[b2], 1u);
-        }
-      }
+      for (int j = 0; j < 4; ++j)
+        if (es[q] + j < ls[q]) atomicAdd(&h[fine_bin(u4get(kk, j), F)], 1u);
     }
   }
   __syncthreads();
-  uint32_t* gha = LEVEL == 1 ? W.hist1 : W.hist2h;
-  for (int b = tid; b < kHistBins; b += kBlock) {
-    if (ha[b]) atomicAdd(&gha[b], ha[b]);
-    if (LEVEL == 2 && hb[b]) atomicAdd(&W.hist2l[b], hb[b]);
+  FC_TR(3);
+  {                                               // flush into this workgroup's shard
+    uint32_t* gh = W.hist1 + (blockIdx.x % kSampleShards) * kHistBins;
+    for (int b = tid; b < kHistBins; b += kBlock)
+      if (h[b]) atomicAdd(&gh[b], h[b]);
   }
-  uint32_t* done = LEVEL == 1 ? &S->a_done : &S->b_done;
-  if (!last_block_arrive_sc1(done, gridDim.x, &s_flag)) return;
-  // ---- last workgroup: resolve the bracket ranks (read + clear the histograms) ----
-  for (int b = tid; b < kHistBins; b += kBlock) {
-    ha[b] = ld_agent(&gha[b]); st_agent(&gha[b], 0u);
-    if (LEVEL == 2) { hb[b] = ld_agent(&W.hist2l[b]); st_agent(&W.hist2l[b], 0u); }
+  FC_TR(4);
+  if (!last_block_arrive_tree(W.tick, gridDim.x, blockIdx.x, &s_flag, 18)) return;
+  FC_TR(5);
+  // ---- last workgroup: the bracket (read + clear the histogram) ----
+  {
+    // every load first (one round trip), then the clearing stores: a load and a store of the
+    // same address issue in order, so interleaving them cost one round trip per bin (~45 us)
+    constexpr int kPer = kHistBins / kBlock;
+    uint32_t t[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) t[j] = 0;
+#pragma unroll
+    for (int sh = 0; sh < kSampleShards; ++sh)
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) t[j] += ld_agent(&W.hist1[sh * kHistBins + j * kBlock + tid]);
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) h[j * kBlock + tid] = t[j];
+#pragma unroll
+    for (int sh = 0; sh < kSampleShards; ++sh)
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) st_agent(&W.hist1[sh * kHistBins + j * kBlock + tid], 0u);
   }
   __syncthreads();
-  if (LEVEL == 1) {
-    uint32_t bh = 0, rh = 1, bl = 0, rl = 1;
-    if (!P.hi_none) { find_rank_desc(ha, (uint32_t)P.r_hi, s_tmp, s_out); bh = s_out[0]; rh = s_out[1]; }
-    if (!P.lo_all) { find_rank_desc(ha, (uint32_t)P.r_lo, s_tmp, s_out); bl = s_out[0]; rl = s_out[1]; }
-    if (tid == 0) {
-      S->b1_hi = bh; S->rr_hi = rh; S->b1_lo = bl; S->rr_lo = rl;
-      S->hi_none = P.hi_none; S->lo_all = P.lo_all; S->a_done = 0;
-    }
-  } else {
-    uint32_t t_hi = 0xffffffffu, t_lo = 0u;
-    if (!hi_none) {
-      find_rank_desc(ha, S->rr_hi, s_tmp, s_out);
-      t_hi = (b1_hi << 19) | (s_out[0] << 7) | 0x7fu;
-    }
-    if (!lo_all) {
-      find_rank_desc(hb, S->rr_lo, s_tmp, s_out);
-      t_lo = (b1_lo << 19) | (s_out[0] << 7);
-    }
-    if (tid < kShards) { S->shard_ent[tid] = 0; S->shard_cnd[tid] = 0; }  // k_compact totals
-    if (tid == 0) {
-      const uint64_t span = (uint64_t)t_hi - t_lo;          // candidate keys: [t_lo, t_hi]
-      uint32_t sb = 0;
-      while ((span >> sb) >= (uint64_t)kHistBins) ++sb;
-      S->t_lo = t_lo; S->t_hi = t_hi; S->sbin = sb; S->L64 = (uint64_t)t_lo << ib;
-      S->cand_on = 1; S->n_cand = 0; S->cand_over = 0; S->ent_over = 0;
-      S->b_done = 0;
-      hdr->lower = (uint64_t)t_lo << ib;
-    }
+  find_ranks_desc(h, P.hi_none ? 1u : (uint32_t)P.r_hi, P.lo_all ? 1u : (uint32_t)P.r_lo, s_tmp, s_out);
+  const uint32_t t_hi = P.hi_none ? 0xffffffffu : fine_upper(s_out[0], F);
+  const uint32_t t_lo = P.lo_all ? 0u : fine_lower(s_out[2], F);
+  if (tid < kShards) { S->shard_ent[tid] = 0; S->shard_cnd[tid] = 0; }  // k_compact totals
+  if (tid == 0) {
+    const uint64_t span = (uint64_t)t_hi - t_lo;          // candidate keys: [t_lo, t_hi]
+    uint32_t sb = 0;
+    while ((span >> sb) >= (uint64_t)kHistBins) ++sb;
+    S->t_lo = t_lo; S->t_hi = t_hi; S->sbin = sb; S->L64 = (uint64_t)t_lo << ib;
+    S->cand_on = 1; S->n_cand = 0; S->cand_over = 0; S->ent_over = 0;
+    S->win_flag = 0;               // (err: set by a timed-out wait, read and
+                                                  // cleared by this call's k_resolve)
+    hdr->lower = (uint64_t)t_lo << ib;
   }
+  FC_TR(6);
 }
 
 
@@ -636,7 +782,7 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
   const uint64_t slot = base;
   // fc_topk_encode_dense: the dense result q = zeros_like(g); q[listed] = g (compression.py:
   // 33-37) leaves with the same coalesced layout as the loads; the slack entries (listed,
-  // comp < T64) are zeroed by k_dense_fixup once k_resolve has T64
+  // comp < T64) are zeroed by k_resolve once it has T64
   auto dense_out = [&](int q, bool p) {
     if (!DENSE) return;                               // uniform
     const uint32_t e = base + FC_LOC(q);
@@ -904,52 +1050,18 @@ __global__ __launch_bounds__(kCBlock, FC_MAG1_WAVES_PER_EU) void k_compact_mag1_
 // with spills at 80-96: DESIGN.md §Lessons.)
 
 // --------------------------------------------------------------------------------------
-// k_dense_fixup (fc_topk_encode_dense, after k_resolve): k_compact_mag1 wrote q = g at every
-// listed element (comp >= L64); the slack ones (comp < T64) go back to +0.  Every slack entry
-// is a candidate (key <= t_hi), so each chunk's candidate slot holds them; a chunk whose
-// candidates overflowed that slot is re-checked from its packet entries (as k_resolve does).
-// A packet whose status is not OK is left alone: the host re-encodes it exactly and decodes.
-// --------------------------------------------------------------------------------------
-struct DenseFixArgs {
-  const fc_packet_hdr* hdr;
-  const uint32_t* idx;
-  const float* val;
-  const uint32_t* cnt;
-  const uint32_t* ccnt;
-  const uint64_t* cand;
-  float* dense;
-  uint32_t ib, nchunks;
-};
-
-__global__ __launch_bounds__(kBlock) void k_dense_fixup(DenseFixArgs a) {
-  if (ld_agent(&a.hdr->status) != FC_STATUS_OK) return;
-  const uint64_t T = ld_agent(&a.hdr->thresh);
-  const uint64_t imask = (1ull << a.ib) - 1;
-  for (uint32_t c = blockIdx.x; c < a.nchunks; c += gridDim.x) {
-    const uint32_t nc = a.ccnt[c];
-    if (nc == 0) continue;
-    if (nc <= (uint32_t)kCandSlot) {
-      for (uint32_t t = threadIdx.x; t < nc; t += blockDim.x) {
-        const uint64_t comp = a.cand[(uint64_t)c * kCandSlot + t];
-        if (comp < T) a.dense[comp & imask] = 0.0f;
-      }
-    } else {
-      const uint32_t ne = a.cnt[c];
-      for (uint32_t e = threadIdx.x; e < ne; e += blockDim.x) {
-        const uint32_t id = a.idx[(uint64_t)c * kChunk + e];
-        const float v = a.val[(uint64_t)c * kChunk + e];
-        if (comp_of(mag_key(v), id, a.ib) < T) a.dense[id] = 0.0f;
-      }
-    }
-  }
-}
-
-// --------------------------------------------------------------------------------------
 // k_resolve: exact T64 from the bracket's candidates (fast path, one launch).
 //   totals from the sharded counters -> rank r = k - #(key > t_hi) -> histogram bin beta
 //   holding rank r -> every workgroup gathers its chunks' candidates that fall in beta
 //   (candidate slot, or the entries slot when the chunk overflowed its candidate slot) ->
 //   the last workgroup sorts the <= 4096 survivors in LDS and picks T64.
+// fc_topk_encode_dense (a.dense set, one client): k_compact_mag1_dense wrote q = g at every
+// LISTED element (comp >= L64); the slack ones (comp < T64) must go back to +0.  Every slack
+// entry is a candidate of its chunk, so the workgroups that gathered a chunk range wait for the
+// last one to publish T64 (generation counter, release/acquire) and zero the slack of their
+// own range: no fix-up launch (it took 13.8 us per 128 M gradient as its own kernel).  The
+// wait is safe: the grid (<= 256 workgroups, 3 per CU by LDS) is always co-resident, and the
+// spin is bounded (FC_STATUS_TIMEOUT, never expected).
 // --------------------------------------------------------------------------------------
 struct ResolveArgs {
   uint32_t ib, nchunks;
@@ -963,6 +1075,7 @@ struct ResolveArgs {
   WsPtrs W;
   const fc_encode_job* jobs;   // batched encode (see CompactArgs)
   uint64_t ws_stride;
+  float* dense;                // fc_topk_encode_dense: zero the slack of q (one client)
 };
 
 constexpr int kResolveChunksMax = 2048;   // chunks per workgroup handled through LDS sizes
@@ -971,84 +1084,114 @@ __global__ __launch_bounds__(kBlock) void k_resolve(ResolveArgs a0) {
   ResolveArgs a = a0;
   apply_job(a);
   __shared__ uint64_t sv[kSmallCap];                      // 32 KiB: histogram, then sort
-  __shared__ uint32_t s_pre[kResolveChunksMax + 1];       // per-chunk gather sizes (prefix)
-  __shared__ uint64_t s_ovf[kResolveChunksMax / 64];      // chunk overflowed its cand slot
-  __shared__ uint32_t s_tmp[8], s_out[4], s_flag, s_cnt, s_base, s_tot[2];
+  __shared__ uint32_t s_pre[kResolveChunksMax];           // per-chunk gather sizes
+  __shared__ uint32_t s_tmp[8], s_out[4], s_flag, s_cnt, s_base, s_tot[2], s_st;
+  __shared__ uint64_t s_T;
   uint32_t* h = reinterpret_cast<uint32_t*>(sv);          // 4096 bins = 16 KiB
   TopkState* S = a.W.st;
   const int tid = threadIdx.x;
-  // ---- totals (sharded counters written by k_compact) ----
-  if (tid < 2) s_tot[tid] = 0;
-  __syncthreads();
-  if (tid < kShards) {
-    atomicAdd(&s_tot[0], S->shard_ent[tid]);
-    atomicAdd(&s_tot[1], S->shard_cnd[tid]);
+  FC_TR(8);
+  const uint32_t gen0 = a.dense ? ld_agent(&S->gen) : 0u; // before the ticket: stable
+  // ---- totals (sharded counters written by k_compact), bracket and candidate histogram:
+  // one round of independent loads (they were three dependent rounds, ~9 us) ----
+  uint32_t se = 0, sc = 0;
+  if (tid < kShards) { se = S->shard_ent[tid]; sc = S->shard_cnd[tid]; }
+  const uint32_t t_lo = S->t_lo, t_hi = S->t_hi, sbin = S->sbin, err = S->err;
+  uint32_t hv[kHistBins / kBlock];
+#pragma unroll
+  for (int j = 0; j < kHistBins / kBlock; ++j) hv[j] = a.W.chist[j * kBlock + tid];
+  static_assert(kShards == 64, "shard totals: one wave");
+  if (tid < 64) {
+    se = wave_sum(se);
+    sc = wave_sum(sc);
+    if (tid == 0) { s_tot[0] = se; s_tot[1] = sc; }
   }
+#pragma unroll
+  for (int j = 0; j < kHistBins / kBlock; ++j) h[j * kBlock + tid] = hv[j];
   __syncthreads();
   const uint32_t n_ent = s_tot[0], n_cand = s_tot[1];
-  const uint32_t t_lo = S->t_lo, t_hi = S->t_hi, sbin = S->sbin;
   const uint32_t n_hi = n_ent - n_cand;                   // listed above the bracket
-  const bool bad = S->err || n_cand > n_ent || (uint64_t)n_ent < a.k || (uint64_t)n_hi > a.k;
+  const bool bad = err || n_cand > n_ent || (uint64_t)n_ent < a.k || (uint64_t)n_hi > a.k;
   const uint32_t rank = bad ? 0u : (uint32_t)(a.k - n_hi);
   bool retry = bad;
   uint32_t beta = 0, r_in = 1, cnt_beta = 0;
   if (!bad && rank > 0) {
-    for (int b = tid; b < kHistBins; b += kBlock) h[b] = a.W.chist[b];
-    __syncthreads();
     find_rank_desc(h, rank, s_tmp, s_out);
     beta = s_out[0]; r_in = s_out[1]; cnt_beta = h[beta];
     retry = cnt_beta > (uint32_t)kSmallCap || cnt_beta < r_in;
     __syncthreads();
   }
+  FC_TR(9);
   const uint32_t per = (a.nchunks + gridDim.x - 1) / gridDim.x;
-  if (!bad && rank > 0 && !retry && per <= (uint32_t)kResolveChunksMax) {
-    // chunk range of this workgroup; gather sizes (candidate slot or, overflowed, entries)
-    const uint32_t c0 = blockIdx.x * per;
-    const uint32_t c1 = min(c0 + per, a.nchunks);
-    const uint32_t nc = c1 > c0 ? c1 - c0 : 0u;
-    uint32_t carry = 0;
-    for (uint32_t b0 = 0; b0 < nc; b0 += kBlock) {
-      const uint32_t c = c0 + b0 + tid;
-      uint32_t sz = 0;
-      bool ovf = false;
-      if (b0 + tid < nc) {
-        const uint32_t cc = a.W.ccnt[c];
-        ovf = cc > (uint32_t)kCandSlot;
-        sz = ovf ? a.cnt[c] : cc;
-      }
-      const uint64_t ob = __ballot(ovf);                // overflow flags, one bit per chunk
-      if ((tid & 63) == 0) s_ovf[(b0 + tid) >> 6] = ob;
-      uint32_t tot;
-      const uint32_t ex = block_excl_scan(sz, s_tmp, &tot);
-      if (b0 + tid < nc) s_pre[b0 + tid] = carry + ex;
-      carry += tot;
+  if (!bad && !retry && per > (uint32_t)kResolveChunksMax) retry = true;   // exact path
+  // chunk range of this workgroup; gather sizes (candidate slot or, overflowed, entries)
+  const uint32_t c0 = blockIdx.x * per;
+  const uint32_t c1 = min(c0 + per, a.nchunks);
+  const uint32_t nc = c1 > c0 ? c1 - c0 : 0u;
+  const bool walk = !retry && (rank > 0 || a.dense);      // uniform
+  // ---- per-chunk gather sizes: the candidate slot, or (bit 31) the entries slot of a chunk
+  // whose candidates overflowed their slot ----
+  if (walk) {
+    for (uint32_t lc = tid; lc < nc; lc += kBlock) {
+      const uint32_t c = c0 + lc;
+      const uint32_t cc = a.W.ccnt[c];
+      s_pre[lc] = cc > (uint32_t)kCandSlot ? (a.cnt[c] | 0x80000000u) : cc;
     }
-    if (tid == 0) { s_pre[nc] = carry; s_cnt = 0; }
     __syncthreads();
-    // gather bin beta into the LDS list (sv reused after the histogram): kGatherU independent
-    // loads per thread in flight, then filter (one dependent global latency per round)
-    constexpr int kGatherU = 8;
-    for (uint32_t j0 = 0; j0 < carry; j0 += kBlock * kGatherU) {
-      uint64_t v[kGatherU];
+  }
+  FC_TR(10);
+  // tpc threads (a power of two) share a chunk and read its candidates kGatherU per thread and
+  // pass, with no search (a binary search over a prefix per candidate cost ~4 us at 128 M)
+  constexpr int kGatherU = 8;
+  uint32_t tpc = 64;
+  while (tpc > 1 && tpc * nc > (uint32_t)kBlock) tpc >>= 1;
+  uint64_t v0[kGatherU];                                  // first pass, kept for the fix-up
 #pragma unroll
-      for (int u = 0; u < kGatherU; ++u) {
-        const uint32_t j = j0 + (uint32_t)(u * kBlock + tid);
-        v[u] = ~0ull;
-        if (j < carry) {
-          uint32_t lo = 0, hi = nc;                   // find chunk: s_pre[lo] <= j < s_pre[lo+1]
-          while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (s_pre[mid] <= j) lo = mid; else hi = mid; }
-          const uint32_t c = c0 + lo, r = j - s_pre[lo];
-          if (!((s_ovf[lo >> 6] >> (lo & 63)) & 1ull)) {
-            v[u] = a.W.cand[(uint64_t)c * kCandSlot + r];
-          } else {
-            const uint64_t p = (uint64_t)c * kChunk + r;
-            const uint32_t id = a.idx[p];
-            const uint32_t key = a.key_mode == FC_KEY_PHILOX ? (philox_word(id, a.seed, a.offset) >> 1)
-                                                             : mag_key(a.val[p]);
-            v[u] = (key >= t_lo && key <= t_hi) ? comp_of(key, id, a.ib) : ~0ull;
+  for (int u = 0; u < kGatherU; ++u) v0[u] = ~0ull;
+  // fn(v) for every pass of this thread over its candidates as comps (~0 = not a candidate:
+  // an overflowed chunk's entry outside [t_lo, t_hi]); reuse: the first pass comes from v0
+  auto for_cands = [&](bool reuse, auto&& fn) {
+    const uint32_t cpr = (uint32_t)kBlock / tpc;
+    for (uint32_t cb = 0; cb < nc; cb += cpr) {
+      const uint32_t lc = cb + (uint32_t)tid / tpc, q = (uint32_t)tid % tpc;
+      const uint32_t info = lc < nc ? s_pre[lc] : 0u;
+      const uint32_t sz = info & 0x7fffffffu;
+      const bool ovf = (info >> 31) != 0;
+      const uint32_t c = c0 + lc;
+      for (uint32_t r0 = q; r0 < sz; r0 += tpc * kGatherU) {
+        const bool first = cb == 0 && r0 == q;
+        uint64_t v[kGatherU];
+#pragma unroll
+        for (int u = 0; u < kGatherU; ++u) {
+          const uint32_t r = r0 + (uint32_t)u * tpc;
+          v[u] = ~0ull;
+          if (reuse && first) {
+            v[u] = v0[u];
+          } else if (r < sz) {
+            if (!ovf) {
+              v[u] = a.W.cand[(uint64_t)c * kCandSlot + r];
+            } else {
+              const uint64_t p = (uint64_t)c * kChunk + r;
+              const uint32_t id = a.idx[p];
+              const uint32_t key = a.key_mode == FC_KEY_PHILOX ? (philox_word(id, a.seed, a.offset) >> 1)
+                                                               : mag_key(a.val[p]);
+              v[u] = (key >= t_lo && key <= t_hi) ? comp_of(key, id, a.ib) : ~0ull;
+            }
           }
         }
+        if (first && !reuse) {
+#pragma unroll
+          for (int u = 0; u < kGatherU; ++u) v0[u] = v[u];
+        }
+        fn(v);
       }
+    }
+  };
+  if (walk && rank > 0) {
+    // gather bin beta into the LDS list (sv reused after the histogram)
+    if (tid == 0) s_cnt = 0;
+    __syncthreads();
+    for_cands(false, [&](const uint64_t (&v)[kGatherU]) {
 #pragma unroll
       for (int u = 0; u < kGatherU; ++u) {
         if (v[u] != ~0ull && ((((uint32_t)(v[u] >> a.ib)) - t_lo) >> sbin) == beta) {
@@ -1056,17 +1199,43 @@ __global__ __launch_bounds__(kBlock) void k_resolve(ResolveArgs a0) {
           if (q < (uint32_t)kSmallCap) sv[q] = v[u];
         }
       }
-    }
+    });
     __syncthreads();
     if (tid == 0 && s_cnt) s_base = atomicAdd(&S->small_n, min(s_cnt, (uint32_t)kSmallCap));
     __syncthreads();
     const uint32_t mine = min(s_cnt, (uint32_t)kSmallCap);
     for (uint32_t q = tid; q < mine; q += kBlock)
       if (s_base + q < (uint32_t)kSmallCap) st_agent(&a.W.small[s_base + q], sv[q]);
-  } else if (!bad && rank > 0 && !retry) {
-    retry = true;                                     // > 2048 chunks per group: exact path
   }
-  if (!last_block_arrive_sc1(&S->r_done, gridDim.x, &s_flag)) return;
+  FC_TR(11);
+  // dense fix-up of this workgroup's range once T64 is known: q[idx] = +0 for comp < T64
+  auto fixup = [&](uint64_t T) {
+    const uint64_t imask = (1ull << a.ib) - 1;
+    for_cands(rank > 0, [&](const uint64_t (&v)[kGatherU]) {
+#pragma unroll
+      for (int u = 0; u < kGatherU; ++u)
+        if (v[u] < T) a.dense[v[u] & imask] = 0.0f;       // ~0 (not a candidate) is never < T
+    });
+  };
+  if (!last_block_arrive_tree(a.W.tick + kTickWords, gridDim.x, blockIdx.x, &s_flag, 16)) {
+    if (!a.dense || !walk) return;
+    if (tid == 0) {                                     // wait for the last workgroup's T64
+      // relaxed sc1 poll; the payload (T_pub, st_pub) is sc1-stored and sc1-loaded, so no
+      // acquire (MI355X_MICROARCH.md: acquire polls by 255 workgroups cut chip bandwidth)
+      uint32_t it = 0;
+      while (ld_agent(&S->gen) == gen0 && ++it < kSpinMax) __builtin_amdgcn_s_sleep(8);
+      const bool ok = it < kSpinMax;
+      s_T = ok ? ld_agent(&S->T_pub) : 0ull;
+      s_st = ok ? ld_agent(&S->st_pub) : (uint32_t)FC_STATUS_TIMEOUT;
+      if (!ok) st_agent(&a.hdr->status, (uint32_t)FC_STATUS_TIMEOUT);
+    }
+    __syncthreads();
+    FC_TR(12);
+    if (s_st == FC_STATUS_OK) fixup(s_T);
+    FC_TR(13);
+    return;
+  }
+  FC_TR(12);
   // ---- last workgroup ----
   uint64_t T = 0;
   uint32_t status = FC_STATUS_OK;
@@ -1076,6 +1245,20 @@ __global__ __launch_bounds__(kBlock) void k_resolve(ResolveArgs a0) {
     T = kSelectNothing;
   } else if (rank == 0) {
     T = ((uint64_t)t_hi + 1) << a.ib;                     // exactly the definite set
+  } else if (cnt_beta <= (uint32_t)kBlock) {
+    // <= 256 candidates: thread i ranks candidate i by counting the larger ones (comps are
+    // unique); the one with r_in - 1 larger ones is T64 — no sort, one barrier
+    __syncthreads();
+    uint64_t mine = 0;
+    if ((uint32_t)tid < cnt_beta) { mine = ld_agent(&a.W.small[tid]); sv[tid] = mine; }
+    __syncthreads();
+    if ((uint32_t)tid < cnt_beta) {
+      uint32_t larger = 0;
+      for (uint32_t j = 0; j < cnt_beta; ++j) larger += sv[j] > mine ? 1u : 0u;
+      if (larger == r_in - 1) s_T = mine;
+    }
+    __syncthreads();
+    T = s_T;
   } else {
     uint32_t P2 = 1;
     while (P2 < cnt_beta) P2 <<= 1;
@@ -1086,6 +1269,13 @@ __global__ __launch_bounds__(kBlock) void k_resolve(ResolveArgs a0) {
     T = sv[r_in - 1];
   }
   __syncthreads();
+  FC_TR(13);
+  if (tid == 0 && a.dense) {                            // publish T64 to the waiting workgroups
+    st_agent(&S->T_pub, T);                             // first: sc1 payload, drained, sc1 flag
+    st_agent(&S->st_pub, status);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    st_agent(&S->gen, gen0 + 1u);
+  }
   for (int b = tid; b < kHistBins; b += kBlock) a.W.chist[b] = 0;   // for the next call
   if (tid == 0) {
     a.hdr->thresh = T;
@@ -1093,8 +1283,11 @@ __global__ __launch_bounds__(kBlock) void k_resolve(ResolveArgs a0) {
     if (status != FC_STATUS_OK) a.hdr->status = status;
     a.hdr->n_definite = n_hi;
     a.hdr->n_cand = n_cand;
-    S->small_n = 0; S->r_done = 0;
+    S->small_n = 0; S->err = 0;
   }
+  FC_TR(14);
+  if (a.dense && walk && status == FC_STATUS_OK) fixup(T);
+  FC_TR(15);
 }
 
 
@@ -1182,7 +1375,7 @@ __global__ __launch_bounds__(kBlock) void k_engine(EngineArgs a) {
   if (!E.done) {
     if (!collect) {
       __syncthreads();
-      for (int b = tid; b < kHistBins; b += kBlock) { h[b] = ld_agent(&a.W.ehist[b]); st_agent(&a.W.ehist[b], 0u); }
+      load_clear_hist(a.W.ehist, h);
       __syncthreads();
       find_rank_desc(h, E.rank, s_tmp, s_out);
       const uint32_t d = s_out[0];
@@ -1225,10 +1418,8 @@ __global__ __launch_bounds__(kBlock) void k_engine(EngineArgs a) {
 // --------------------------------------------------------------------------------------
 // explicit instantiations used by fc_capi.hip
 // --------------------------------------------------------------------------------------
-template __global__ void k_sample<kKeyMag, 1>(const float*, SamplePlan, uint64_t, uint64_t, WsPtrs, uint32_t, fc_packet_hdr*, HdrInit, const fc_encode_job*, uint64_t);
-template __global__ void k_sample<kKeyMag, 2>(const float*, SamplePlan, uint64_t, uint64_t, WsPtrs, uint32_t, fc_packet_hdr*, HdrInit, const fc_encode_job*, uint64_t);
-template __global__ void k_sample<kKeyPhilox, 1>(const float*, SamplePlan, uint64_t, uint64_t, WsPtrs, uint32_t, fc_packet_hdr*, HdrInit, const fc_encode_job*, uint64_t);
-template __global__ void k_sample<kKeyPhilox, 2>(const float*, SamplePlan, uint64_t, uint64_t, WsPtrs, uint32_t, fc_packet_hdr*, HdrInit, const fc_encode_job*, uint64_t);
+template __global__ void k_sample1<kKeyMag>(const float*, SamplePlan, uint64_t, uint64_t, WsPtrs, uint32_t, fc_packet_hdr*, HdrInit, const fc_encode_job*, uint64_t);
+template __global__ void k_sample1<kKeyPhilox>(const float*, SamplePlan, uint64_t, uint64_t, WsPtrs, uint32_t, fc_packet_hdr*, HdrInit, const fc_encode_job*, uint64_t);
 template __global__ void k_compact<kKeyMag, kPredKey, FC_FMT_IDXVAL>(CompactArgs);
 template __global__ void k_compact<kKeyPhilox, kPredKey, FC_FMT_IDXVAL>(CompactArgs);
 template __global__ void k_compact<kKeyMag, kPredMask, FC_FMT_IDXVAL>(CompactArgs);

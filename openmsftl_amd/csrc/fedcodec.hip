@@ -3,4 +3,5 @@
 #include "fc_topk.hip"
 #include "fc_decode.hip"
 #include "fc_qsgd.hip"
+#include "fc_f64.hip"
 #include "fc_capi.hip"

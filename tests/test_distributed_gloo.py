@@ -33,7 +33,7 @@ def _oracle_fold(all_rows):
         for j, i in enumerate(rows):
             c = np.multiply(all_rows[i], w[j])
             if j == 0 and not continue_sum:
-                acc[:] = c
+                acc[:] = np.add(np.zeros_like(c), c)      # np.sum's +0 start (gar.py:44)
             else:
                 acc[:] = np.add(acc, c)
         return out
