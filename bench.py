@@ -12,9 +12,12 @@ aggregate to rank 0.  Weak scaling: per-GPU work is fixed.
     torchrun --nproc-per-node N ... bench.py --gpus N       (one process per GPU, RCCL)
 
 Prints ONE JSON line on rank 0.  `value` = gradient bytes (4 N per client, all ranks) per
-second of step time; `roofline` = the encode pass k_compact (the dominant kernel), algorithmic
-bytes 4N + 8k per launch over its HIP-event-timed average duration; `cpu_baseline` = the
-NumPy restatement of compression.py (oracle, same NumPy calls) on one 128 M gradient.
+second of step time; `roofline` = the encode pass k_compact_mag1 (the dominant kernel), algorithmic
+bytes 4N + 8k per client over its HIP-event-timed average launch duration, `traffic` from the
+committed calibrated PMC summary; `cpu_baseline` = the reference's exact NumPy calls
+(compression.py:31-37, default argsort) on one 128 M gradient, with every BASELINE.md §3 row
+in `extra.cpu_baseline_matrix`.  A self-check outside the timed region re-encodes two clients
+alone and compares them bit for bit with the batch.
 """
 from __future__ import annotations
 
@@ -34,8 +37,8 @@ HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--clients", type=int, default=128, help="clients per GPU")
     ap.add_argument("--n", type=int, default=134_217_728, help="gradient length (fp32)")
     ap.add_argument("--fraction", type=float, default=0.1)
@@ -47,7 +50,7 @@ def parse():
     ap.add_argument("--no-single", action="store_true", help="skip the single-gradient probe")
     ap.add_argument("--no-batch", action="store_true",
                     help="encode client by client (fc_topk_encode) instead of batched")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01_pmc_k_compact_mag1.json"),
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r02_pmc_k_compact_mag1.json"),
                     help="PMC summary (profiles/) used for roofline.traffic")
     return ap.parse_args()
 
@@ -70,31 +73,98 @@ def make_grads(M, n, rank, device, torch):
     return grads
 
 
+def _timed(fn):
+    t0 = time.perf_counter()
+    out = fn()
+    return out, time.perf_counter() - t0
+
+
 def cpu_baseline(n, fraction):
-    """Oracle (NumPy restatement, same calls as compression.py:31-37) on one client gradient."""
+    """The reference's own top-k call on one client gradient: oracle/compression_oracle.py with
+    ``argsort_kind=None``, i.e. exactly compression.py:31-37 (np.zeros_like, round(f*N),
+    np.argsort(np.abs(g)) with NumPy's DEFAULT kind, [::-1][:k], scatter), single-threaded."""
     import numpy as np
     from oracle import compression_oracle as co
     g = np.random.default_rng(0).standard_normal(n, dtype=np.float32)
     g *= np.float32(1e-2)
     cfg = {"compression_function": "top", "fraction_coordinate": fraction}
-    t0 = time.perf_counter()
-    q = co.compress(cfg, g)
-    dt = time.perf_counter() - t0
+    q, dt = _timed(lambda: co.compress(cfg, g, argsort_kind=None))
     assert q.shape == g.shape
     return {"value": round(4.0 * n / dt / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
-            "sample": f"1 client x {n:,} fp32, top f={fraction}: oracle/compression_oracle.py "
-                      f"(NumPy argsort, same calls as compression.py:31-37), single-threaded; "
-                      f"{dt:.2f} s on {os.cpu_count()} visible host cores"}
+            "sample": f"1 client x {n:,} fp32, top f={fraction}: the reference's exact NumPy "
+                      f"calls (compression.py:31-37, default-kind argsort; "
+                      f"oracle/compression_oracle.py argsort_kind=None), single-threaded; "
+                      f"{dt:.2f} s on {os.cpu_count()} visible host cores (1 used)"}
+
+
+def cpu_matrix(n16=16_777_216, n25=25_557_032):
+    """every codec of compression.py:23-77 and gar.py:44's FedAvg, the
+    reference's exact NumPy calls (oracle, default argsort kind, legacy np.random), one core,
+    on a bounded sample (one 16 M / 25.5 M client, 4 x 16 M for FedAvg), plus the per-config
+    CPU time extrapolated linearly in clients."""
+    import numpy as np
+    from oracle import compression_oracle as co
+    from oracle import gar_oracle as go
+    g = np.random.default_rng(1).standard_normal(n16, dtype=np.float32) * np.float32(1e-2)
+    rows = {}
+
+    def row(name, cfg, grad, seed=0):
+        np.random.seed(seed)
+        _, dt = _timed(lambda: co.compress(cfg, grad, argsort_kind=None))
+        rows[name] = {"ms": round(1e3 * dt, 1), "GBps": round(4.0 * grad.shape[0] / dt / 1e9, 4),
+                      "n": int(grad.shape[0])}
+        return dt
+
+    t_top16 = row("top_f0.1_16M", {"compression_function": "top", "fraction_coordinate": 0.1}, g)
+    row("top_f0.01_16M", {"compression_function": "top", "fraction_coordinate": 0.01}, g)
+    row("rand_f0.1_16M", {"compression_function": "rand", "fraction_coordinate": 0.1}, g)
+    row("dropout-biased_p0.1_16M", {"compression_function": "dropout-biased", "dropout_p": 0.1}, g)
+    row("dropout-unbiased_p0.1_16M", {"compression_function": "dropout-unbiased", "dropout_p": 0.1}, g)
+    rows["full_16M"] = {"ms": 0.0, "GBps": None, "n": n16,
+                        "note": "compression.py:27-29 returns the caller's array (no work)"}
+    g25 = np.random.default_rng(2).standard_normal(n25, dtype=np.float32) * np.float32(1e-2)
+    t_top25 = row("top_f0.01_25.5M", {"compression_function": "top", "fraction_coordinate": 0.01}, g25)
+    del g25
+    G = np.stack([g * np.float32(0.5 ** i) for i in range(4)])
+    _, t_avg4 = _timed(lambda: go.FedAvgOracle({}).aggregate(G))
+    rows["fedavg_4x16M"] = {"ms": round(1e3 * t_avg4, 1), "GBps_of_G": round(G.nbytes / t_avg4 / 1e9, 4)}
+    per_row = t_avg4 / 4                            # FedAvg cost per 16 M row
+    extrap = {
+        "configs1_1x16M_top0.1_s": round(t_top16, 2),
+        "configs2_128x16M_top0.1_fedavg_s": round(128 * (t_top16 + per_row), 1),
+        "configs3_per_gpu_128x128M_top0.1_fedavg_s": None,      # filled from the headline client
+        "configs4_per_gpu_512x25.5M_top0.01_fedavg_s": round(512 * (t_top25 + per_row * n25 / n16), 1),
+        "method": "clients x (one timed client + one row of the timed 4 x 16 M FedAvg, scaled by N)",
+    }
+    return {"rows": rows, "extrapolated": extrap, "per_row_fedavg_16M_s": per_row,
+            "cores": 1, "kind": "port (the reference's NumPy calls; default argsort kind)"}
+
+
+def self_check(torch, codec, grads, pkts, k):
+    """Outside the timed region: clients 0 and 1 re-encoded ALONE (fc_topk_encode) give the
+    batched packets' dense result bit for bit (compression.py:31-37 per client)."""
+    ok = True
+    for i in (0, 1):
+        single = codec.encode_top(grads[i], k)
+        a = codec.decode(single).view(torch.int32)
+        b = codec.decode(pkts[i]).view(torch.int32)
+        ok = ok and bool(torch.equal(a, b))
+        del single, a, b
+    if not ok:
+        raise SystemExit("self-check failed: batched encode differs from a single-client encode")
+    return "ok: clients 0, 1 re-encoded singly, dense results bit-identical to the batch"
 
 
 def load_pmc(path):
-    """HBM bytes per client of k_compact, from the committed rocprofv3 PMC summary."""
+    """HBM bytes per client of k_compact_mag1 from the committed rocprofv3 PMC summary
+    (tools/pmc_round.sh: FETCH_SIZE / WRITE_SIZE at 128 clients per launch, calibrated on known
+    byte counts of the same access shapes)."""
     try:
         with open(path) as fh:
             d = json.load(fh)
-        return d["hbm_bytes_per_launch"] / d.get("clients_per_launch", 1)
+        return d["hbm_bytes_per_launch"] / d.get("clients_per_launch", 1), os.path.relpath(path, ROOT)
     except (OSError, ValueError, KeyError):
-        return None
+        return None, None
 
 
 def main():
@@ -195,12 +265,13 @@ def main():
     # the encode pass reads 4N and writes 8k per client
     alg_bytes = per_launch * (4.0 * n + 8.0 * k)
     achieved = alg_bytes / (t_compact_us * 1e-6) / 1e9
-    pmc = load_pmc(args.pmc)
+    pmc, pmc_src = load_pmc(args.pmc)
     roofline = {"kernel": "fc::k_compact_mag1 (top-k encode pass, %d client(s) per launch)"
                           % per_launch, "bound": "hbm",
                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": int(pmc * per_launch) if pmc else None,
+                "traffic_source": pmc_src,
                 "alg_bytes_per_launch": int(alg_bytes), "avg_launch_us": round(t_compact_us, 2),
                 "launches": kt_roof.launches.get("compact", 0),
                 "measured": "one-stream encode passes after the timed steps"
@@ -220,6 +291,7 @@ def main():
              "step_roofline": {"alg_bytes_per_gpu": int(step_alg),
                                "achieved_GBps": round(step_gbps, 1),
                                "frac": round(step_gbps / world / HBM_PEAK_GBPS, 4)}}
+    extra["self_check"] = self_check(torch, codec, grads, pkts, k)
     if rank == 0 and not args.no_single:
         extra["single_gradient"] = single_gradient(torch, codec, grads[0], k, n)
         extra["qsgd_single_gradient"] = qsgd_single(torch, codec, grads[0], n)
@@ -234,6 +306,11 @@ def main():
     cpu = None
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
         cpu = cpu_baseline(n, f)
+        mat = cpu_matrix()
+        t_client = 4.0 * n / (cpu["value"] * 1e9)
+        mat["extrapolated"]["configs3_per_gpu_128x128M_top0.1_fedavg_s"] = round(
+            M * (t_client + mat.pop("per_row_fedavg_16M_s") * n / 16_777_216), 1)
+        extra["cpu_baseline_matrix"] = mat
 
     if rank == 0:
         line = {

@@ -37,7 +37,7 @@ extern "C" {
 
 typedef void* fc_stream_t; /* hipStream_t */
 
-#define FC_ABI_VERSION 1
+#define FC_ABI_VERSION 2
 
 /* return codes */
 #define FC_OK 0
@@ -71,8 +71,13 @@ typedef void* fc_stream_t; /* hipStream_t */
  * entries (ascending index order) live at [c*FC_CHUNK, c*FC_CHUNK + cnt[c]) of idx/val (and
  * its bitmap words at [c*256, c*256+256)).  Every chunk is encoded by an independent
  * workgroup — no global scan — so buffers are sized fc_packet_capacity(n) entries while only
- * the listed entries are written or read. */
+ * the listed entries are written or read.
+ * FC_FMT_IDXVAL packets also carry qoff[c] (uint64 per chunk): the slot positions where the
+ * chunk's four quarters (FC_CHUNK/4 elements each) begin — quarter 1, 2, 3 in bits 0-15,
+ * 16-31, 32-47 — and cnt[c] in bits 48-63, so a decoder can hand each quarter to its own wave
+ * (fc_decode_accumulate requires it). */
 #define FC_CHUNK 8192        /* elements per chunk */
+#define FC_QUARTER (FC_CHUNK / 4)
 
 /* Device-resident packet header (96 bytes). */
 typedef struct fc_packet_hdr {
@@ -95,13 +100,14 @@ typedef struct fc_packet_hdr {
   uint32_t reserved[3];
 } fc_packet_hdr;
 
-/* One packet as seen by the decoders (host- or device-resident array element, 48 bytes). */
+/* One packet as seen by the decoders (host- or device-resident array element, 56 bytes). */
 typedef struct fc_packet_view {
   const uint32_t* idx;          /* FC_FMT_IDXVAL                        */
   const float* val;
   const uint32_t* bitmap;       /* FC_FMT_BITMAP                        */
   const uint32_t* cnt;          /* ceil(N/FC_CHUNK) entries per chunk   */
   const fc_packet_hdr* hdr;
+  const uint64_t* qoff;         /* FC_FMT_IDXVAL: quarter offsets per chunk (see above) */
   float weight;                 /* FedAVG weight w_i (gar.py:37-44)     */
   uint32_t reserved;
 } fc_packet_view;
@@ -122,10 +128,11 @@ int fc_workspace_init(void* ws, size_t ws_bytes, fc_stream_t stream);
  * chunk's slot (one launch, independent workgroups), then the exact k-th composite key is
  * resolved from the bracket's candidates.  hdr->status == FC_STATUS_RETRY_EXACT means the
  * bracket missed (adversarial / tie-heavy data): call fc_topk_encode_exact with the same
- * arguments.  capacity >= fc_packet_capacity(n); cnt has fc_num_chunks(n) words. */
+ * arguments.  capacity >= fc_packet_capacity(n); cnt and qoff have fc_num_chunks(n) words
+ * (qoff may be NULL: not written, and the packet cannot be folded by fc_decode_accumulate). */
 int fc_topk_encode(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_t seed,
                    uint64_t offset, uint32_t* idx, float* val, uint64_t capacity,
-                   uint32_t* cnt, fc_packet_hdr* hdr, void* ws, size_t ws_bytes,
+                   uint32_t* cnt, uint64_t* qoff, fc_packet_hdr* hdr, void* ws, size_t ws_bytes,
                    fc_stream_t stream);
 /* ---- top-k straight to the dense result (compression.py:31-37 returns q, not a packet) --
  * The fc_topk_encode pipeline (magnitude keys) whose compaction pass also streams
@@ -134,8 +141,8 @@ int fc_topk_encode(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_
  * header reports FC_STATUS_RETRY_EXACT, `dense` is not valid: re-encode with
  * fc_topk_encode_exact and fc_decode_dense (as for a packet).  Needs 0 < k < n. */
 int fc_topk_encode_dense(const float* g, uint64_t n, uint64_t k, uint32_t* idx, float* val,
-                         uint64_t capacity, uint32_t* cnt, fc_packet_hdr* hdr, void* ws,
-                         size_t ws_bytes, float* dense, fc_stream_t stream);
+                         uint64_t capacity, uint32_t* cnt, uint64_t* qoff, fc_packet_hdr* hdr,
+                         void* ws, size_t ws_bytes, float* dense, fc_stream_t stream);
 /* ---- batched top-k / native rand-k: M clients, one launch per pipeline stage ----------
  * The same fast path as fc_topk_encode for m gradients of equal length n, with the grid's
  * y dimension indexing the client: 4 launches for the whole batch instead of 4 per client,
@@ -151,7 +158,7 @@ typedef struct fc_encode_job {
   fc_packet_hdr* hdr;
   uint64_t seed;         /* Philox key / counter (FC_KEY_PHILOX)            */
   uint64_t offset;
-  uint64_t reserved;
+  uint64_t* qoff;        /* quarter offsets per chunk (may be NULL)         */
 } fc_encode_job;         /* 64 bytes */
 size_t fc_workspace_bytes_batch(uint64_t n, int m);
 int fc_topk_encode_batch(const fc_encode_job* jobs_dev, int m, uint64_t n, uint64_t k,
@@ -161,18 +168,20 @@ int fc_topk_encode_batch(const fc_encode_job* jobs_dev, int m, uint64_t n, uint6
 /* Exact radix-select path (several reads of g); always succeeds; n_entries == k. */
 int fc_topk_encode_exact(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_t seed,
                          uint64_t offset, uint32_t* idx, float* val, uint64_t capacity,
-                         uint32_t* cnt, fc_packet_hdr* hdr, void* ws, size_t ws_bytes,
-                         fc_stream_t stream);
+                         uint32_t* cnt, uint64_t* qoff, fc_packet_hdr* hdr, void* ws,
+                         size_t ws_bytes, fc_stream_t stream);
 
 /* ---- encode: mask codecs (compression.py:39-60) -------------------------------------
  * codec = FC_CODEC_DROPOUT_* or FC_CODEC_RAND (parity mode: mask from the host's
  * np.random.permutation).  mask_bits (little-endian bit i = element i, N/32 words) is the
  * host-drawn mask in parity mode; NULL selects native Philox Bernoulli(p) keyed by seed.
- * format: FC_FMT_BITMAP (bitmap required) or FC_FMT_IDXVAL (idx required). */
+ * format: FC_FMT_BITMAP (bitmap required) or FC_FMT_IDXVAL (idx required; qoff written when
+ * non-NULL). */
 int fc_mask_encode(const float* g, uint64_t n, int codec, const uint32_t* mask_bits,
                    double p, uint64_t seed, uint64_t offset, int format, uint32_t* idx,
                    float* val, uint32_t* bitmap, uint64_t capacity, uint32_t* cnt,
-                   fc_packet_hdr* hdr, void* ws, size_t ws_bytes, fc_stream_t stream);
+                   uint64_t* qoff, fc_packet_hdr* hdr, void* ws, size_t ws_bytes,
+                   fc_stream_t stream);
 
 /* ---- decode (compression.py dense result) --------------------------------------------
  * pkt: HOST pointer to one view.  out is float (out_f64 = 0) or double (out_f64 = 1; the
@@ -181,7 +190,8 @@ int fc_decode_dense(const fc_packet_view* pkt, int format, uint64_t n, void* out
                     fc_stream_t stream);
 
 /* ---- FedAVG over packets (aggregation.py:61-63 + gar.py:44), bit-exact fp32 ----------
- * views: DEVICE array of m views (same format), client order = row order of G.
+ * views: DEVICE array of m views (same format), client order = row order of G; FC_FMT_IDXVAL
+ * views must carry qoff (each chunk quarter is folded by its own wave, no barriers).
  * acc[j] = fl(w_0 * d_0[j]);  acc[j] = fl(acc[j] + fl(w_i * d_i[j])) for i = 1..m-1. */
 int fc_decode_accumulate(const fc_packet_view* views_dev, int m, int format, uint64_t n,
                          float* acc, fc_stream_t stream);

@@ -46,20 +46,20 @@ class PacketHdr(ctypes.Structure):
 class PacketView(ctypes.Structure):
     _fields_ = [("idx", ctypes.c_void_p), ("val", ctypes.c_void_p),
                 ("bitmap", ctypes.c_void_p), ("cnt", ctypes.c_void_p),
-                ("hdr", ctypes.c_void_p), ("weight", ctypes.c_float),
-                ("reserved", ctypes.c_uint32)]
+                ("hdr", ctypes.c_void_p), ("qoff", ctypes.c_void_p),
+                ("weight", ctypes.c_float), ("reserved", ctypes.c_uint32)]
 
 
 class EncodeJob(ctypes.Structure):
     _fields_ = [("g", ctypes.c_void_p), ("idx", ctypes.c_void_p), ("val", ctypes.c_void_p),
                 ("cnt", ctypes.c_void_p), ("hdr", ctypes.c_void_p),
                 ("seed", ctypes.c_uint64), ("offset", ctypes.c_uint64),
-                ("reserved", ctypes.c_uint64)]
+                ("qoff", ctypes.c_void_p)]
 
 
 assert ctypes.sizeof(PacketHdr) == HDR_BYTES
 assert ctypes.sizeof(EncodeJob) == 64
-assert ctypes.sizeof(PacketView) == 48
+assert ctypes.sizeof(PacketView) == 56
 
 _u64, _i32, _sz, _vp, _dbl = (ctypes.c_uint64, ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p,
                               ctypes.c_double)
@@ -73,15 +73,15 @@ SIGNATURES = {
     "fc_packet_capacity": (_u64, [_u64]),
     "fc_workspace_init": (_i32, [_vp, _sz, _vp]),
     "fc_topk_encode": (_i32, [_vp, _u64, _u64, _i32, _u64, _u64, _vp, _vp, _u64, _vp, _vp,
-                              _vp, _sz, _vp]),
-    "fc_topk_encode_dense": (_i32, [_vp, _u64, _u64, _vp, _vp, _u64, _vp, _vp, _vp, _sz, _vp,
-                                    _vp]),
+                              _vp, _vp, _sz, _vp]),
+    "fc_topk_encode_dense": (_i32, [_vp, _u64, _u64, _vp, _vp, _u64, _vp, _vp, _vp, _vp, _sz,
+                                    _vp, _vp]),
     "fc_workspace_bytes_batch": (_sz, [_u64, _i32]),
     "fc_topk_encode_batch": (_i32, [_vp, _i32, _u64, _u64, _i32, _u64, _vp, _sz, _vp]),
     "fc_topk_encode_exact": (_i32, [_vp, _u64, _u64, _i32, _u64, _u64, _vp, _vp, _u64, _vp,
-                                    _vp, _vp, _sz, _vp]),
+                                    _vp, _vp, _vp, _sz, _vp]),
     "fc_mask_encode": (_i32, [_vp, _u64, _i32, _vp, _dbl, _u64, _u64, _i32, _vp, _vp, _vp,
-                              _u64, _vp, _vp, _vp, _sz, _vp]),
+                              _u64, _vp, _vp, _vp, _vp, _sz, _vp]),
     "fc_decode_dense": (_i32, [ctypes.POINTER(PacketView), _i32, _u64, _vp, _i32, _vp]),
     "fc_decode_accumulate": (_i32, [_vp, _i32, _i32, _u64, _vp, _vp]),
     "fc_decode_accumulate_continue": (_i32, [_vp, _i32, _i32, _u64, _vp, _vp]),
@@ -151,7 +151,7 @@ def load(path: str = LIB_PATH):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        if lib.fc_abi_version() != 1:
+        if lib.fc_abi_version() != 2:
             raise FedCodecUnavailable("libfedcodec.so ABI mismatch")
         _lib = lib
         return lib

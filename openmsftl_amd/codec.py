@@ -79,6 +79,7 @@ class Packet:
     idx: Optional[torch.Tensor] = None
     bitmap: Optional[torch.Tensor] = None
     k: int = 0
+    qoff: Optional[torch.Tensor] = None    # int64[num_chunks]: quarter offsets (FC_FMT_IDXVAL)
 
     @classmethod
     def alloc(cls, n: int, fmt: int, device, hdr: Optional[torch.Tensor] = None,
@@ -93,7 +94,9 @@ class Packet:
                                                                device=device),
                    idx=torch.empty(cap, dtype=_U32, device=device) if fmt == L.FC_FMT_IDXVAL else None,
                    bitmap=torch.empty(nch * 256, dtype=_U32, device=device)
-                   if fmt == L.FC_FMT_BITMAP else None)
+                   if fmt == L.FC_FMT_BITMAP else None,
+                   qoff=torch.empty(nch, dtype=torch.int64, device=device)
+                   if fmt == L.FC_FMT_IDXVAL else None)
 
     @property
     def capacity(self) -> int:
@@ -109,6 +112,7 @@ class Packet:
                             val=self.val.data_ptr(),
                             bitmap=self.bitmap.data_ptr() if self.bitmap is not None else 0,
                             cnt=self.cnt.data_ptr(), hdr=self.hdr.data_ptr(),
+                            qoff=self.qoff.data_ptr() if self.qoff is not None else 0,
                             weight=float(np.float32(weight)), reserved=0)
 
     def header(self) -> L.PacketHdr:
@@ -160,8 +164,8 @@ def encode_top(g: torch.Tensor, k: int, *, key_mode: int = L.FC_KEY_MAGNITUDE, s
     packet.k = k
     fn = lib.fc_topk_encode_exact if exact else lib.fc_topk_encode
     L.check(fn(_vp(g), n, k, key_mode, seed, offset, _vp(packet.idx), _vp(packet.val),
-               packet.capacity, _vp(packet.cnt), _vp(packet.hdr), _vp(ws.buf), ws.nbytes,
-               _stream(g.device)), "fc_topk_encode")
+               packet.capacity, _vp(packet.cnt), _vp(packet.qoff), _vp(packet.hdr), _vp(ws.buf),
+               ws.nbytes, _stream(g.device)), "fc_topk_encode")
     packet._enc = (g, k, key_mode, seed, offset)
     if check:
         resolve([packet])
@@ -191,9 +195,9 @@ def compress_top_dense(g: torch.Tensor, k: int, out: Optional[torch.Tensor] = No
     ws = Workspace.get(n, g.device)
     packet.k = k
     L.check(lib.fc_topk_encode_dense(_vp(g), n, k, _vp(packet.idx), _vp(packet.val),
-                                     packet.capacity, _vp(packet.cnt), _vp(packet.hdr),
-                                     _vp(ws.buf), ws.nbytes, _vp(out), _stream(g.device)),
-            "fc_topk_encode_dense")
+                                     packet.capacity, _vp(packet.cnt), _vp(packet.qoff),
+                                     _vp(packet.hdr), _vp(ws.buf), ws.nbytes, _vp(out),
+                                     _stream(g.device)), "fc_topk_encode_dense")
     packet._enc = (g, k, L.FC_KEY_MAGNITUDE, 0, 0)
     if check and resolve([packet]):            # bracket missed: exact packet, then decode
         decode(packet, out=out)
@@ -246,7 +250,7 @@ def encode_jobs(grads: Sequence[torch.Tensor], packets: Sequence[Packet], seeds=
     arr = (L.EncodeJob * m)(*[
         L.EncodeJob(g=g.data_ptr(), idx=p.idx.data_ptr(), val=p.val.data_ptr(),
                     cnt=p.cnt.data_ptr(), hdr=p.hdr.data_ptr(), seed=int(s), offset=int(o),
-                    reserved=0)
+                    qoff=p.qoff.data_ptr() if p.qoff is not None else 0)
         for g, p, s, o in zip(grads, packets, seeds, offsets)])
     host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
     return host.to(grads[0].device)
@@ -344,7 +348,7 @@ def resolve(packets: Sequence[Packet]) -> int:
         ws = Workspace.get(g.numel(), g.device)
         L.check(lib.fc_topk_encode_exact(_vp(g), g.numel(), k, key_mode, seed, offset,
                                          _vp(p.idx), _vp(p.val), p.capacity, _vp(p.cnt),
-                                         _vp(p.hdr), _vp(ws.buf), ws.nbytes,
+                                         _vp(p.qoff), _vp(p.hdr), _vp(ws.buf), ws.nbytes,
                                          _stream(g.device)), "fc_topk_encode_exact")
         redo += 1
         h2 = p.header()
@@ -370,8 +374,9 @@ def encode_mask(g: torch.Tensor, codec: int, *, p: float = 0.5,
         packet = Packet.alloc(n, fmt, g.device)
     L.check(lib.fc_mask_encode(_vp(g), n, codec, _vp(mask_bits), float(p), seed, offset, fmt,
                                _vp(packet.idx), _vp(packet.val), _vp(packet.bitmap),
-                               packet.capacity, _vp(packet.cnt), _vp(packet.hdr), _vp(ws.buf),
-                               ws.nbytes, _stream(g.device)), "fc_mask_encode")
+                               packet.capacity, _vp(packet.cnt), _vp(packet.qoff),
+                               _vp(packet.hdr), _vp(ws.buf), ws.nbytes, _stream(g.device)),
+            "fc_mask_encode")
     return packet
 
 

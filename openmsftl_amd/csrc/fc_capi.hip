@@ -259,8 +259,9 @@ int fc_workspace_init(void* ws, size_t ws_bytes, fc_stream_t stream) {
 
 static int topk_args(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_t seed,
                      uint64_t offset, uint32_t* idx, float* val, uint64_t capacity,
-                     uint32_t* cnt, fc_packet_hdr* hdr, void* ws, size_t ws_bytes,
-                     CompactArgs* ca, EngineArgs* ea, ResolveArgs* ra, HdrInit* hi) {
+                     uint32_t* cnt, uint64_t* qoff, fc_packet_hdr* hdr, void* ws,
+                     size_t ws_bytes, CompactArgs* ca, EngineArgs* ea, ResolveArgs* ra,
+                     HdrInit* hi) {
   int rc = check_common(g, n, ws, ws_bytes);
   if (rc) return rc;
   FC_CHECK(idx && val && cnt && hdr, "packet buffers must be non-NULL");
@@ -277,6 +278,7 @@ static int topk_args(const float* g, uint64_t n, uint64_t k, int key_mode, uint6
   memset(ca, 0, sizeof *ca);
   ca->g = g; ca->n = n; ca->ib = ib; ca->nchunks = num_chunks(n);
   ca->seed = seed; ca->offset = offset; ca->idx = idx; ca->val = val; ca->cnt = cnt;
+  ca->qoff = qoff;
   ca->hdr = hdr; ca->W = ws_ptrs(ws, n); ca->HI = *hi;
   memset(ea, 0, sizeof *ea);
   ea->g = g; ea->n = n; ea->ib = ib; ea->k = k;
@@ -290,10 +292,10 @@ static int topk_args(const float* g, uint64_t n, uint64_t k, int key_mode, uint6
 
 int fc_topk_encode_exact(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_t seed,
                          uint64_t offset, uint32_t* idx, float* val, uint64_t capacity,
-                         uint32_t* cnt, fc_packet_hdr* hdr, void* ws, size_t ws_bytes,
-                         fc_stream_t stream) {
+                         uint32_t* cnt, uint64_t* qoff, fc_packet_hdr* hdr, void* ws,
+                         size_t ws_bytes, fc_stream_t stream) {
   CompactArgs ca; EngineArgs ea; ResolveArgs ra; HdrInit hi;
-  int rc = topk_args(g, n, k, key_mode, seed, offset, idx, val, capacity, cnt, hdr, ws,
+  int rc = topk_args(g, n, k, key_mode, seed, offset, idx, val, capacity, cnt, qoff, hdr, ws,
                      ws_bytes, &ca, &ea, &ra, &hi);
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
@@ -304,13 +306,13 @@ int fc_topk_encode_exact(const float* g, uint64_t n, uint64_t k, int key_mode, u
 
 int fc_topk_encode(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_t seed,
                    uint64_t offset, uint32_t* idx, float* val, uint64_t capacity,
-                   uint32_t* cnt, fc_packet_hdr* hdr, void* ws, size_t ws_bytes,
-                   fc_stream_t stream) {
+                   uint32_t* cnt, uint64_t* qoff, fc_packet_hdr* hdr, void* ws,
+                   size_t ws_bytes, fc_stream_t stream) {
   if (k == 0 || k >= n)  // trivial thresholds: the exact engine resolves them in its init
-    return fc_topk_encode_exact(g, n, k, key_mode, seed, offset, idx, val, capacity, cnt, hdr,
-                                ws, ws_bytes, stream);
+    return fc_topk_encode_exact(g, n, k, key_mode, seed, offset, idx, val, capacity, cnt, qoff,
+                                hdr, ws, ws_bytes, stream);
   CompactArgs ca; EngineArgs ea; ResolveArgs ra; HdrInit hi;
-  int rc = topk_args(g, n, k, key_mode, seed, offset, idx, val, capacity, cnt, hdr, ws,
+  int rc = topk_args(g, n, k, key_mode, seed, offset, idx, val, capacity, cnt, qoff, hdr, ws,
                      ws_bytes, &ca, &ea, &ra, &hi);
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
@@ -324,13 +326,13 @@ int fc_topk_encode(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_
 }
 
 int fc_topk_encode_dense(const float* g, uint64_t n, uint64_t k, uint32_t* idx, float* val,
-                         uint64_t capacity, uint32_t* cnt, fc_packet_hdr* hdr, void* ws,
-                         size_t ws_bytes, float* dense, fc_stream_t stream) {
+                         uint64_t capacity, uint32_t* cnt, uint64_t* qoff, fc_packet_hdr* hdr,
+                         void* ws, size_t ws_bytes, float* dense, fc_stream_t stream) {
   FC_CHECK(dense != nullptr, "dense is NULL");
   FC_CHECK(((uintptr_t)dense & 15) == 0, "dense must be 16-byte aligned");
   FC_CHECK(k > 0 && k < n, "fc_topk_encode_dense needs 0 < k < n (trivial k: encode + decode)");
   CompactArgs ca; EngineArgs ea; ResolveArgs ra; HdrInit hi;
-  int rc = topk_args(g, n, k, FC_KEY_MAGNITUDE, 0, 0, idx, val, capacity, cnt, hdr, ws,
+  int rc = topk_args(g, n, k, FC_KEY_MAGNITUDE, 0, 0, idx, val, capacity, cnt, qoff, hdr, ws,
                      ws_bytes, &ca, &ea, &ra, &hi);
   if (rc) return rc;
   ca.dense = dense;
@@ -409,8 +411,8 @@ int fc_topk_encode_batch(const fc_encode_job* jobs, int m, uint64_t n, uint64_t 
 
 int fc_mask_encode(const float* g, uint64_t n, int codec, const uint32_t* mask_bits, double p,
                    uint64_t seed, uint64_t offset, int format, uint32_t* idx, float* val,
-                   uint32_t* bitmap, uint64_t capacity, uint32_t* cnt, fc_packet_hdr* hdr,
-                   void* ws, size_t ws_bytes, fc_stream_t stream) {
+                   uint32_t* bitmap, uint64_t capacity, uint32_t* cnt, uint64_t* qoff,
+                   fc_packet_hdr* hdr, void* ws, size_t ws_bytes, fc_stream_t stream) {
   int rc = check_common(g, n, ws, ws_bytes);
   if (rc) return rc;
   FC_CHECK(codec == FC_CODEC_DROPOUT_BIASED || codec == FC_CODEC_DROPOUT_UNBIASED ||
@@ -438,6 +440,7 @@ int fc_mask_encode(const float* g, uint64_t n, int codec, const uint32_t* mask_b
   a.bern_thr = (uint64_t)thr;
   a.nonfinite_keep = codec != FC_CODEC_RAND;
   a.write_hdr = 1; a.idx = idx; a.val = val; a.bitmap = bitmap; a.cnt = cnt;
+  a.qoff = format == FC_FMT_IDXVAL ? qoff : nullptr;
   a.hdr = hdr; a.W = ws_ptrs(ws, n); a.HI = hi;
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid(a.nchunks), blk(kCBlock);
@@ -499,11 +502,13 @@ static int decode_accumulate(const fc_packet_view* views_dev, int m, int format,
     a.views = views_dev + m0; a.m = std::min(m - m0, per_launch); a.acc_in = cont || m0 > 0;
     a.n = n; a.out = acc;
     TimedLaunch t(FC_TIME_DECODE, s);
-    if (format == FC_FMT_IDXVAL)
-      // fold: one WG per chunk (16384 at 128 M), not persistent: 23.4 -> 22.3 us per packet
-      // over 128 distinct packets (no tail of unequal per-WG chunk counts)
-      hipLaunchKernelGGL(k_decode_sparse<true>, dim3(decode_grid(n, 1u << 20)), dim3(kSBlock), 0, s, a);
-    else hipLaunchKernelGGL((k_decode<FC_FMT_BITMAP, true, false>), grid, blk, 0, s, a);
+    if (format == FC_FMT_IDXVAL) {
+      // fold: one workgroup per chunk, each wave folding its own quarter (no barriers)
+      if (a.acc_in) hipLaunchKernelGGL(k_fold_q<true>, dim3(num_chunks(n)), dim3(kQBlock), 0, s, a);
+      else hipLaunchKernelGGL(k_fold_q<false>, dim3(num_chunks(n)), dim3(kQBlock), 0, s, a);
+    } else {
+      hipLaunchKernelGGL((k_decode<FC_FMT_BITMAP, true, false>), grid, blk, 0, s, a);
+    }
     FC_LAUNCHED("k_decode(acc)");
   }
   return FC_OK;

@@ -187,12 +187,7 @@ __device__ __forceinline__ uint32_t spread4(uint32_t x) {
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_tmp,
                                                     uint32_t* total) {
   const int lane = lane_id(), w = threadIdx.x >> 6;
-  uint32_t inc = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t t = __shfl_up(inc, o, 64);
-    if (lane >= o) inc += t;
-  }
+  const uint32_t inc = wave_incl_scan(v);          // DPP: 6 fused adds, no LDS round trips
   if (lane == 63) s_tmp[w] = inc;
   __syncthreads();
   uint32_t base = 0, tot = 0;

@@ -760,6 +760,213 @@ __global__ __launch_bounds__(kSBlock, kSBlocksPerCU) void k_decode_sparse(Decode
 }
 #endif
 
+// --------------------------------------------------------------------------------------
+// k_fold_q: the FedAVG fold of FC_FMT_IDXVAL packets (aggregation.py:61-63 + gar.py:44) with
+// quarter ownership.  One workgroup of 4 waves per chunk; wave q owns quarter q (2048 elements,
+// an 8 KB LDS tile) and folds every packet's entries of that quarter in G's row order,
+//     tile[loc] = fl(tile[loc] + fl(w * v))           (__fmul_rn / __fadd_rn, no FMA)
+// with NO barrier: the quarter's entries are the slot range [qoff_q, qoff_q+1) the encoder
+// recorded (include/fedcodec.h), a packet's locations are distinct, and one wave's LDS
+// operations execute in order.  (k_decode_sparse<true> shared one tile among the 4 waves and
+// paid a workgroup barrier per (packet, chunk): 2.73 ms per 128 packets of 128 M.)
+// The chunk's quarter offsets of all M packets are loaded once, one packet per lane, and read
+// back with readlane; entries are loaded in groups of kQGroup items, two groups in flight.
+// +0 start, skipped dropped coordinates and NaN-poisoning packets: see k_decode_sparse.
+// --------------------------------------------------------------------------------------
+constexpr int kQBlock = 256;
+constexpr int kQuarter = kChunk / 4;
+#ifndef FC_QR
+#define FC_QR 5
+#endif
+constexpr int kQR = FC_QR;                      // entry rounds (x64 lanes) loaded per item: 320
+                                                // entries, ~8 sigma above a quarter at f = 0.1
+#ifndef FC_QG
+#define FC_QG 3
+#endif
+constexpr int kQGroup = FC_QG;                  // items per load group
+
+struct QMeta {
+  const uint32_t* idx;
+  const float* val;
+  const uint64_t* qoff;
+  const fc_packet_hdr* hdr;
+  uint64_t thresh;
+  float w;
+  uint32_t flags;                               // ib | codec << 8 | key_mode << 16 | poison << 24
+};
+
+// One entry of a packet folded into the quarter tile with the full per-entry rules (the slow
+// body): rand-k (Philox keys) slack filter, dropout-unbiased fl32(fl64(v)/p) scaling.
+__device__ __forceinline__ void fold_q_entry(const PktCache& pk, float w, float* qt,
+                                             uint32_t qbase, uint32_t id, float v) {
+  if (!entry_kept(pk, id, v)) return;
+  const float x = pk.codec == FC_CODEC_DROPOUT_UNBIASED ? (float)((double)v / pk.p) : v;
+  const uint32_t loc = id - qbase;
+  if (loc < (uint32_t)kQuarter) qt[loc] = __fadd_rn(qt[loc], __fmul_rn(x, w));
+}
+
+template <bool ACC_IN>
+__global__ __launch_bounds__(kQBlock, 4) void k_fold_q(DecodeArgs a) {
+  __shared__ __attribute__((aligned(16))) float tile[kChunk];
+  __shared__ QMeta s_meta[kSparseMaxM];
+  __shared__ uint32_t s_mark[4][kQuarter / 32];   // poisoning packets: kept-location bits
+  __shared__ uint32_t s_slow;
+  const int tid = threadIdx.x, lane = lane_id(), q = tid >> 6;
+  const uint32_t M = (uint32_t)a.m;
+  const uint32_t c = blockIdx.x;
+  const uint64_t base = (uint64_t)c * kChunk;
+  const uint32_t qbase = (uint32_t)base + (uint32_t)(q * kQuarter);
+  if (tid == 0) s_slow = 0;
+  s_mark[q][lane] = 0u;
+  __syncthreads();
+  if (tid < (int)M) {
+    const fc_packet_view v = a.views[tid];
+    const fc_packet_hdr* h = v.hdr;
+    QMeta d;
+    d.idx = v.idx; d.val = v.val; d.qoff = v.qoff; d.hdr = h;
+    d.thresh = h->thresh; d.w = v.weight;
+    const uint32_t codec = h->codec, key_mode = h->key_mode;
+    const float dz = (codec == FC_CODEC_DROPOUT_UNBIASED && h->p == 0.0) ? __uint_as_float(0x7fc00000u) : 0.0f;
+    const bool poison = __fmul_rn(dz, v.weight) != __fmul_rn(dz, v.weight);
+    const bool generic = codec == FC_CODEC_DROPOUT_UNBIASED || (key_mode == FC_KEY_PHILOX && d.thresh != 0);
+    d.flags = (h->index_bits & 0xffu) | ((codec & 0xffu) << 8) | ((key_mode & 0xffu) << 16) |
+              ((uint32_t)poison << 24);
+    s_meta[tid] = d;
+    if (poison || generic) atomicOr(&s_slow, 1u);
+  }
+  __syncthreads();                              // the only workgroup barriers
+  const bool slow = s_slow != 0;
+  // this chunk's quarter offsets of packets lane and lane + 64
+  // (a per-lane pointer: each lane reads a different packet's array)
+  typedef __attribute__((address_space(1))) const uint64_t gu64;
+  const uint64_t qo0 = (uint32_t)lane < M ? ((gu64*)s_meta[lane].qoff)[c] : 0ull;
+  const uint64_t qo1 = (uint32_t)lane + 64 < M ? ((gu64*)s_meta[lane + 64].qoff)[c] : 0ull;
+  // a quarter holding more than kQR * 64 entries in any packet sends this wave to the slow
+  // body too: the fast body has no tail loop (a load loop inside the pipeline made the
+  // compiler wait vmcnt(0) for the other slot's loads)
+  auto qcount = [&](uint64_t v) -> uint32_t {
+    const uint32_t st = q == 0 ? 0u : (uint32_t)(v >> (16 * (q - 1))) & 0xffffu;
+    const uint32_t en = q == 3 ? (uint32_t)(v >> 48) : (uint32_t)(v >> (16 * q)) & 0xffffu;
+    return en - st;
+  };
+  const bool dense_q = __any(qcount(qo0) > (uint32_t)(kQR * 64) || qcount(qo1) > (uint32_t)(kQR * 64));
+  auto range = [&](uint32_t m, uint32_t& st, uint32_t& en) {   // uniform
+    const uint64_t src = m < 64 ? qo0 : qo1;
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)src, (int)(m & 63));
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(src >> 32), (int)(m & 63));
+    const uint64_t v = ((uint64_t)hi << 32) | lo;
+    st = q == 0 ? 0u : (uint32_t)(v >> (16 * (q - 1))) & 0xffffu;
+    en = q == 3 ? (uint32_t)(v >> 48) : (uint32_t)(v >> (16 * q)) & 0xffffu;
+  };
+  // ---- tile init: +0 (np.sum's start) or the partial sum being continued ----
+  float* qt = tile + q * kQuarter;
+#pragma unroll
+  for (int i = 0; i < kQuarter / 256; ++i) {
+    const uint32_t loc = (uint32_t)(i * 256 + lane * 4);
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (ACC_IN) v = load4(reinterpret_cast<const float*>(a.out), (uint64_t)qbase + loc, a.n);
+    *reinterpret_cast<float4*>(&qt[loc]) = v;
+  }
+  if (slow || dense_q) {
+    // ---- slow body (a launch holding rand-k Philox, dropout-unbiased or NaN-poisoning
+    // packets, or a quarter with more than kQR * 64 entries): item by item, every rule per
+    // entry ----
+    for (uint32_t m = 0; m < M; ++m) {
+      uint32_t st, en;
+      range(m, st, en);
+      const QMeta& pm = s_meta[m];
+      const fc_packet_hdr* h = (const fc_packet_hdr*)uni_ptr(pm.hdr);
+      PktCache pk;
+      pk.thresh = uni64(pm.thresh); pk.ib = uni32(pm.flags) & 0xffu;
+      pk.codec = (uni32(pm.flags) >> 8) & 0xffu; pk.key_mode = (uni32(pm.flags) >> 16) & 0xffu;
+      pk.seed = h->seed; pk.offset = h->offset; pk.p = h->p;
+      const float w = __uint_as_float(uni32(__float_as_uint(pm.w)));
+      gu32* pidx = (gu32*)uni_ptr(pm.idx) + base;
+      gf32* pval = (gf32*)uni_ptr(pm.val) + base;
+      if (uni32(pm.flags) >> 24) {              // poisoning: NaN where this packet folds nothing
+        for (uint32_t e = st + lane; e < en; e += 64) {
+          const uint32_t id = pidx[e];
+          const uint32_t loc = id - qbase;
+          if (loc < (uint32_t)kQuarter && entry_kept(pk, id, pval[e]))
+            atomicOr(&s_mark[q][loc >> 5], 1u << (loc & 31));
+        }
+        const uint32_t bits = s_mark[q][lane];
+        for (int b = 0; b < 32; ++b)
+          if (!((bits >> b) & 1u)) qt[lane * 32 + b] = __uint_as_float(0x7fc00000u);
+        s_mark[q][lane] = 0u;
+      }
+      for (uint32_t e = st + lane; e < en; e += 64) fold_q_entry(pk, w, qt, qbase, pidx[e], pval[e]);
+    }
+  } else {
+    // ---- fast body: top-k / mask-selected packets; two register slots of kQGroup items, the
+    // loads of one group in flight while the other is folded (every wait a partial vmcnt) ----
+    uint32_t ids_[2][kQGroup][kQR];
+    float vs_[2][kQGroup][kQR];
+    uint32_t st_[2][kQGroup], en_[2][kQGroup];
+    auto issue = [&](int sl, uint32_t m0) {
+#pragma unroll
+      for (int d = 0; d < kQGroup; ++d) {
+        const uint32_t m = min(m0 + (uint32_t)d, M - 1);          // past the end: re-load (ignored)
+        uint32_t st, en;
+        range(m, st, en);
+        st_[sl][d] = st; en_[sl][d] = en;
+        const QMeta& pm = s_meta[m];
+        gf32* val = (gf32*)uni_ptr(pm.val) + base;
+        gu32* idx = (gu32*)uni_ptr(pm.idx) + base;
+        const uint32_t last = en > st ? en - 1 : st;
+#pragma unroll
+        for (int r = 0; r < kQR; ++r) {
+          const uint32_t e = min(st + (uint32_t)(lane + r * 64), last);
+          vs_[sl][d][r] = val[e];
+          ids_[sl][d][r] = idx[e];
+        }
+      }
+    };
+    auto process = [&](int sl, uint32_t m0) {
+#pragma unroll
+      for (int d = 0; d < kQGroup; ++d) {
+        const uint32_t m = m0 + (uint32_t)d;
+        if (m >= M) break;                                        // uniform
+        const QMeta& pm = s_meta[m];
+        const float w = __uint_as_float(uni32(__float_as_uint(pm.w)));
+        const uint64_t thresh = uni64(pm.thresh);
+        const uint32_t ib = uni32(pm.flags) & 0xffu;
+        const uint32_t st = st_[sl][d], en = en_[sl][d];
+        uint32_t loc[kQR];
+        bool ok[kQR];
+        float tv[kQR];
+#pragma unroll
+        for (int r = 0; r < kQR; ++r) {                           // all tile reads, then writes
+          const uint32_t id = ids_[sl][d][r];
+          const float v = vs_[sl][d][r];
+          loc[r] = id - qbase;
+          ok[r] = st + (uint32_t)(lane + r * 64) < en && loc[r] < (uint32_t)kQuarter &&
+                  (thresh == 0 || comp_of(mag_key(v), id, ib) >= thresh);
+          tv[r] = ok[r] ? qt[loc[r]] : 0.f;
+        }
+#pragma unroll
+        for (int r = 0; r < kQR; ++r)
+          if (ok[r]) qt[loc[r]] = __fadd_rn(tv[r], __fmul_rn(vs_[sl][d][r], w));
+      }
+    };
+    issue(0, 0);
+    for (uint32_t m0 = 0; m0 < M; m0 += 2 * kQGroup) {
+      issue(1, m0 + kQGroup);
+      process(0, m0);
+      if (m0 + kQGroup >= M) break;                                // uniform
+      issue(0, m0 + 2 * kQGroup);
+      process(1, m0 + kQGroup);
+    }
+  }
+  // ---- write the quarter out ----
+  float* out = reinterpret_cast<float*>(a.out);
+#pragma unroll
+  for (int i = 0; i < kQuarter / 256; ++i) {
+    const uint32_t loc = (uint32_t)(i * 256 + lane * 4);
+    store_out(out, (uint64_t)qbase + loc, a.n, *reinterpret_cast<const float4*>(&qt[loc]));
+  }
+}
+
 // Dense FedAVG over M row pointers (gar.py:44 with 'full' rows): one float4 per thread.
 __global__ __launch_bounds__(kBlock) void k_wsum(const float* const* rows, const float* w,
                                                  int m, uint64_t n, float* out) {
@@ -831,6 +1038,8 @@ template __global__ void k_decode<FC_FMT_BITMAP, false, false>(DecodeArgs);
 template __global__ void k_decode<FC_FMT_BITMAP, false, true>(DecodeArgs);
 template __global__ void k_decode<FC_FMT_IDXVAL, true, false>(DecodeArgs);
 template __global__ void k_decode_sparse<true>(DecodeArgs);
+template __global__ void k_fold_q<false>(DecodeArgs);
+template __global__ void k_fold_q<true>(DecodeArgs);
 template __global__ void k_decode_sparse<false>(DecodeArgs);
 template __global__ void k_decode<FC_FMT_BITMAP, true, false>(DecodeArgs);
 

@@ -25,6 +25,8 @@
 // largest comps are kept <=> argsort(|g|, stable)[::-1][:k] (highest index first in a tie),
 // NaN above +inf.  The packet lists every element with comp >= L64 (L64 <= T64); decoders
 // keep comp >= T64.
+#include <type_traits>
+
 #include "fc_state.h"
 
 namespace fc {
@@ -320,10 +322,6 @@ __global__ __launch_bounds__(kBlock) void k_sample1(const float* __restrict__ g,
       for (int j = 0; j < kPer; ++j) t[j] += ld_agent(&W.hist1[sh * kHistBins + j * kBlock + tid]);
 #pragma unroll
     for (int j = 0; j < kPer; ++j) h[j * kBlock + tid] = t[j];
-#pragma unroll
-    for (int sh = 0; sh < kSampleShards; ++sh)
-#pragma unroll
-      for (int j = 0; j < kPer; ++j) st_agent(&W.hist1[sh * kHistBins + j * kBlock + tid], 0u);
   }
   __syncthreads();
   find_ranks_desc(h, P.hi_none ? 1u : (uint32_t)P.r_hi, P.lo_all ? 1u : (uint32_t)P.r_lo, s_tmp, s_out);
@@ -340,6 +338,10 @@ __global__ __launch_bounds__(kBlock) void k_sample1(const float* __restrict__ g,
                                                   // cleared by this call's k_resolve)
     hdr->lower = (uint64_t)t_lo << ib;
   }
+  // clear the shards for the next call last, with plain 16-B stores (their next use is an
+  // atomic in the next launch, after this kernel's end-of-launch write-back)
+  for (int i = tid; i < kHistBins * kSampleShards / 4; i += kBlock)
+    reinterpret_cast<uint4*>(W.hist1)[i] = make_uint4(0u, 0u, 0u, 0u);
   FC_TR(6);
 }
 
@@ -374,6 +376,7 @@ struct CompactArgs {
   float* val;
   uint32_t* bitmap;
   uint32_t* cnt;            // entries per chunk
+  uint64_t* qoff;           // quarter offsets per chunk (include/fedcodec.h), may be null
   fc_packet_hdr* hdr;
   WsPtrs W;
   HdrInit HI;
@@ -388,6 +391,7 @@ __device__ __forceinline__ void apply_job(Args& a) {
   if (!a.jobs) return;
   const fc_encode_job& J = a.jobs[blockIdx.y];
   a.idx = J.idx; a.val = J.val; a.cnt = J.cnt; a.hdr = J.hdr;
+  if constexpr (std::is_same<Args, CompactArgs>::value) a.qoff = J.qoff;
   a.seed = J.seed; a.offset = J.offset;
   a.W = ws_shift(a.W, (uint64_t)blockIdx.y * a.ws_stride);
 }
@@ -533,9 +537,15 @@ __global__ __launch_bounds__(kCBlock, FC_COMPACT_WAVES_PER_EU) void k_compact(Co
     const uint32_t ie = wave_incl_scan(ve);
     const uint32_t ic = PRED == kPredKey ? wave_incl_scan(vc) : 0u;
     if (lane < kCSlots) { s_ent[lane] = ie - ve; if (PRED == kPredKey) s_cnd[lane] = ic - vc; }
+    // quarter q of the chunk = slots (q, w): its entries start where slot (q, 0) does
+    const uint32_t q1 = (uint32_t)__builtin_amdgcn_readlane((int)(ie - ve), 1 * kCWaves);
+    const uint32_t q2 = (uint32_t)__builtin_amdgcn_readlane((int)(ie - ve), 2 * kCWaves);
+    const uint32_t q3 = (uint32_t)__builtin_amdgcn_readlane((int)(ie - ve), 3 * kCWaves);
     if (lane == kCSlots - 1) {
       s_tot[0] = ie; s_tot[1] = ic;
       a.cnt[chunk] = ie;
+      if (FMT == FC_FMT_IDXVAL && a.qoff)
+        a.qoff[chunk] = q1 | ((uint64_t)q2 << 16) | ((uint64_t)q3 << 32) | ((uint64_t)ie << 48);
       if (PRED == kPredKey) {
         a.W.ccnt[chunk] = ic;
         atomicAdd(&S->shard_ent[chunk % kShards], ie);
@@ -723,6 +733,7 @@ struct MagOut {
   uint32_t* idx;
   float* val;
   uint32_t* cnt;
+  uint64_t* qoff;
   TopkState* S;
   uint32_t* ccnt;
   uint64_t* cand;
@@ -768,6 +779,10 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
   const uint32_t incl = wave_incl_scan(sum4);
   const uint32_t tot_e = (uint32_t)__builtin_amdgcn_readlane((int)incl, kMGroups / 4 - 1);
   const uint32_t e0 = incl - sum4;
+  // quarter q of the chunk = words (q, w): its entries start where word (q, 0) does
+  const uint32_t qs1 = (uint32_t)__builtin_amdgcn_readlane((int)e0, 1 * NW);
+  const uint32_t qs2 = (uint32_t)__builtin_amdgcn_readlane((int)e0, 2 * NW);
+  const uint32_t qs3 = (uint32_t)__builtin_amdgcn_readlane((int)e0, 3 * NW);
   const uint32_t e1 = e0 + (word & 0xffu), e2 = e1 + ((word >> 8) & 0xffu);
   const uint32_t e3 = e2 + ((word >> 16) & 0xffu);
   const uint32_t o01 = e0 | (e1 << 16), o23 = e2 | (e3 << 16);
@@ -788,7 +803,7 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
     const uint32_t e = base + FC_LOC(q);
     if (!FAST && e >= P.n32) return;                    // partial last chunk
     const float v = p ? (FAST ? x[q] : a.g[e]) : 0.0f;
-    __builtin_nontemporal_store(v, a.dense + e);
+    __builtin_nontemporal_store(v, a.dense + e);   // (sc1 / plain stores: 269 vs 192 us)
   };
   if (tot_e <= (uint32_t)SH::kStageN) {                 // block-uniform
 #pragma unroll
@@ -838,6 +853,7 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
   if (tid == 0) {
     TopkState* S = a.S;
     a.cnt[chunk] = tot_e;
+    if (a.qoff) a.qoff[chunk] = qs1 | ((uint64_t)qs2 << 16) | ((uint64_t)qs3 << 32) | ((uint64_t)tot_e << 48);
     a.ccnt[chunk] = tot_c;
     atomicAdd(&S->shard_ent[chunk % kShards], tot_e);
     if (tot_c) atomicAdd(&S->shard_cnd[chunk % kShards], tot_c);
@@ -900,12 +916,14 @@ __device__ __forceinline__ TopkState* mag_S(const CompactArgs& a0, uint32_t clie
 __device__ __forceinline__ MagOut mag_out(const CompactArgs& a0, uint32_t client) {
   MagOut o;
   const WsPtrs W = a0.jobs ? ws_shift(a0.W, (uint64_t)client * a0.ws_stride) : a0.W;
-  o.g = a0.g; o.idx = a0.idx; o.val = a0.val; o.cnt = a0.cnt;
+  o.g = a0.g; o.idx = a0.idx; o.val = a0.val; o.cnt = a0.cnt; o.qoff = a0.qoff;
   o.dense = a0.jobs ? nullptr : a0.dense;
   if (a0.jobs) {                                // {g, idx, val, cnt} = first 32 B of the job
     const fc_u32x8 v = sload8(&a0.jobs[client]);
     o.g = as_ptr<const float>(v[0], v[1]); o.idx = as_ptr<uint32_t>(v[2], v[3]);
     o.val = as_ptr<float>(v[4], v[5]); o.cnt = as_ptr<uint32_t>(v[6], v[7]);
+    const fc_u32x2 qv = sload2(&a0.jobs[client].qoff);
+    o.qoff = as_ptr<uint64_t>(qv.x, qv.y);
   }
   o.S = W.st; o.ccnt = W.ccnt; o.cand = W.cand; o.chist = W.chist; o.ib = a0.ib;
   return o;
@@ -980,6 +998,7 @@ __device__ __forceinline__ void compact_mag_item(const CompactArgs& a0, const Ma
     SH::barrier();
     if (tid == 0) {
       o.cnt[chunk] = 0;
+      if (o.qoff) o.qoff[chunk] = 0;
       o.ccnt[chunk] = 0;
     }
     if (DENSE)
@@ -1217,65 +1236,60 @@ __global__ __launch_bounds__(kBlock) void k_resolve(ResolveArgs a0) {
         if (v[u] < T) a.dense[v[u] & imask] = 0.0f;       // ~0 (not a candidate) is never < T
     });
   };
-  if (!last_block_arrive_tree(a.W.tick + kTickWords, gridDim.x, blockIdx.x, &s_flag, 16)) {
+  // T64 from the gathered list: thread i ranks candidate i by counting the larger ones (comps
+  // are unique; <= 256 candidates) or, for a larger bin, an LDS bitonic sort
+  auto select_T = [&]() -> uint64_t {
+    if (retry) return 0ull;
+    if (a.k == 0) return kSelectNothing;
+    if (rank == 0) return ((uint64_t)t_hi + 1) << a.ib;  // exactly the definite set
+    __syncthreads();
+    if (cnt_beta <= (uint32_t)kBlock) {
+      uint64_t mine = 0;
+      if ((uint32_t)tid < cnt_beta) { mine = ld_agent(&a.W.small[tid]); sv[tid] = mine; }
+      __syncthreads();
+      if ((uint32_t)tid < cnt_beta) {
+        uint32_t larger = 0;
+        for (uint32_t j = 0; j < cnt_beta; ++j) larger += sv[j] > mine ? 1u : 0u;
+        if (larger == r_in - 1) s_T = mine;
+      }
+      __syncthreads();
+      return s_T;
+    }
+    uint32_t P2 = 1;
+    while (P2 < cnt_beta) P2 <<= 1;
+    for (uint32_t i = tid; i < P2; i += kBlock) sv[i] = i < cnt_beta ? ld_agent(&a.W.small[i]) : 0ull;
+    __syncthreads();
+    bitonic_desc(sv, P2);
+    return sv[r_in - 1];
+  };
+  const bool last = last_block_arrive_tree(a.W.tick + kTickWords, gridDim.x, blockIdx.x, &s_flag, 16);
+  if (last) {
+    // every workgroup has gathered: say so at once (dense: the others select T64 themselves
+    // from the same list instead of waiting for this one to sort and publish)
+    if (tid == 0 && a.dense) st_agent(&S->gen, gen0 + 1u);
+  } else {
     if (!a.dense || !walk) return;
-    if (tid == 0) {                                     // wait for the last workgroup's T64
-      // relaxed sc1 poll; the payload (T_pub, st_pub) is sc1-stored and sc1-loaded, so no
-      // acquire (MI355X_MICROARCH.md: acquire polls by 255 workgroups cut chip bandwidth)
+    if (tid == 0) {                                     // relaxed sc1 poll (bounded)
       uint32_t it = 0;
-      while (ld_agent(&S->gen) == gen0 && ++it < kSpinMax) __builtin_amdgcn_s_sleep(8);
-      const bool ok = it < kSpinMax;
-      s_T = ok ? ld_agent(&S->T_pub) : 0ull;
-      s_st = ok ? ld_agent(&S->st_pub) : (uint32_t)FC_STATUS_TIMEOUT;
-      if (!ok) st_agent(&a.hdr->status, (uint32_t)FC_STATUS_TIMEOUT);
+      while (ld_agent(&S->gen) == gen0 && ++it < kSpinMax) __builtin_amdgcn_s_sleep(4);
+      s_st = it < kSpinMax ? 0u : 1u;
+      if (it >= kSpinMax) st_agent(&a.hdr->status, (uint32_t)FC_STATUS_TIMEOUT);
     }
     __syncthreads();
     FC_TR(12);
-    if (s_st == FC_STATUS_OK) fixup(s_T);
+    if (s_st != 0) return;
+    const uint64_t T = select_T();
+    FC_TR(14);
+    if (!retry) fixup(T);
     FC_TR(13);
     return;
   }
   FC_TR(12);
   // ---- last workgroup ----
-  uint64_t T = 0;
-  uint32_t status = FC_STATUS_OK;
-  if (retry) {
-    status = FC_STATUS_RETRY_EXACT;
-  } else if (a.k == 0) {
-    T = kSelectNothing;
-  } else if (rank == 0) {
-    T = ((uint64_t)t_hi + 1) << a.ib;                     // exactly the definite set
-  } else if (cnt_beta <= (uint32_t)kBlock) {
-    // <= 256 candidates: thread i ranks candidate i by counting the larger ones (comps are
-    // unique); the one with r_in - 1 larger ones is T64 — no sort, one barrier
-    __syncthreads();
-    uint64_t mine = 0;
-    if ((uint32_t)tid < cnt_beta) { mine = ld_agent(&a.W.small[tid]); sv[tid] = mine; }
-    __syncthreads();
-    if ((uint32_t)tid < cnt_beta) {
-      uint32_t larger = 0;
-      for (uint32_t j = 0; j < cnt_beta; ++j) larger += sv[j] > mine ? 1u : 0u;
-      if (larger == r_in - 1) s_T = mine;
-    }
-    __syncthreads();
-    T = s_T;
-  } else {
-    uint32_t P2 = 1;
-    while (P2 < cnt_beta) P2 <<= 1;
-    __syncthreads();
-    for (uint32_t i = tid; i < P2; i += kBlock) sv[i] = i < cnt_beta ? ld_agent(&a.W.small[i]) : 0ull;
-    __syncthreads();
-    bitonic_desc(sv, P2);
-    T = sv[r_in - 1];
-  }
-  __syncthreads();
-  FC_TR(13);
-  if (tid == 0 && a.dense) {                            // publish T64 to the waiting workgroups
-    st_agent(&S->T_pub, T);                             // first: sc1 payload, drained, sc1 flag
-    st_agent(&S->st_pub, status);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    st_agent(&S->gen, gen0 + 1u);
-  }
+  const uint64_t T = select_T();
+  const uint32_t status = retry ? (uint32_t)FC_STATUS_RETRY_EXACT : (uint32_t)FC_STATUS_OK;
+  FC_TR(14);
+  if (a.dense && walk && !retry) fixup(T);
   for (int b = tid; b < kHistBins; b += kBlock) a.W.chist[b] = 0;   // for the next call
   if (tid == 0) {
     a.hdr->thresh = T;
@@ -1285,8 +1299,6 @@ __global__ __launch_bounds__(kBlock) void k_resolve(ResolveArgs a0) {
     a.hdr->n_cand = n_cand;
     S->small_n = 0; S->err = 0;
   }
-  FC_TR(14);
-  if (a.dense && walk && status == FC_STATUS_OK) fixup(T);
   FC_TR(15);
 }
 

@@ -37,13 +37,16 @@ def effective_k(k: int, n: int) -> int:
     return len(range(n)[:k])
 
 
-def topk_indices(grad: np.ndarray, k: int) -> np.ndarray:
-    """compression.py:35 with the build's tie rule (stable argsort, reversed)."""
-    return np.argsort(np.abs(grad), kind="stable")[::-1][:k]
+def topk_indices(grad: np.ndarray, k: int, kind: str | None = "stable") -> np.ndarray:
+    """compression.py:35 with the build's tie rule (stable argsort, reversed).  ``kind=None``
+    is the reference's exact call (NumPy's default introsort; ties implementation-defined):
+    the timed CPU baseline uses it, parity checks never do."""
+    return np.argsort(np.abs(grad), kind=kind)[::-1][:k]
 
 
-def compress(cfg: dict, grad, layer_wise: bool = False, rng=np.random):
-    """compression.py:23-77.  ``rng`` defaults to the process-global legacy ``np.random``."""
+def compress(cfg: dict, grad, layer_wise: bool = False, rng=np.random, argsort_kind="stable"):
+    """compression.py:23-77.  ``rng`` defaults to the process-global legacy ``np.random``;
+    ``argsort_kind=None`` times the reference's own argsort call (bench.py cpu_baseline)."""
     func, _num_bits, frac, p = config_fields(cfg)
     if layer_wise:                                     # :24-25
         raise NotImplementedError
@@ -52,7 +55,7 @@ def compress(cfg: dict, grad, layer_wise: bool = False, rng=np.random):
     if func == "top":                                  # :31-37
         q = np.zeros_like(grad)
         k = num_kept(frac, q.shape[0])
-        idx = topk_indices(grad, k)
+        idx = topk_indices(grad, k, argsort_kind)
         q[idx] = grad[idx]
         return q
     if func == "rand":                                 # :39-45

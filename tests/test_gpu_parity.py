@@ -28,7 +28,7 @@ def _gpu():
         pytest.skip("no GPU")
     from openmsftl_amd import _lib
     lib = _lib.load()
-    assert lib.fc_abi_version() == 1
+    assert lib.fc_abi_version() == 2
 
 
 def _codec():

@@ -52,9 +52,11 @@ def test_lib_is_gfx950_only():
 def test_struct_layouts():
     from openmsftl_amd import _lib
     assert ctypes.sizeof(_lib.PacketHdr) == 96
-    assert ctypes.sizeof(_lib.PacketView) == 48
+    assert ctypes.sizeof(_lib.PacketView) == 56
     assert _lib.PacketHdr.p.offset == 64 and _lib.PacketHdr.seed.offset == 48
-    assert _lib.PacketView.cnt.offset == 24 and _lib.PacketView.weight.offset == 40
+    assert _lib.PacketView.cnt.offset == 24 and _lib.PacketView.qoff.offset == 40
+    assert _lib.PacketView.weight.offset == 48
+    assert ctypes.sizeof(_lib.EncodeJob) == 64 and _lib.EncodeJob.qoff.offset == 56
 
 
 def test_sizes_are_host_functions(lib):
@@ -67,14 +69,14 @@ def test_sizes_are_host_functions(lib):
 
 def test_argument_errors_do_not_touch_gpu(lib):
     from openmsftl_amd import _lib
-    rc = lib.fc_topk_encode(None, 10, 1, 0, 0, 0, None, None, 10, None, None, None, 0, None)
+    rc = lib.fc_topk_encode(None, 10, 1, 0, 0, 0, None, None, 10, None, None, None, None, 0, None)
     assert rc == -1 and b"g is NULL" in lib.fc_last_error()
     buf = ctypes.create_string_buffer(64)
     addr = (ctypes.addressof(buf) + 15) & ~15
-    rc = lib.fc_topk_encode(addr, 10, 1, 0, 0, 0, addr, addr, 10, addr, addr, addr, 16, None)
+    rc = lib.fc_topk_encode(addr, 10, 1, 0, 0, 0, addr, addr, 10, addr, addr, addr, addr, 16, None)
     assert rc == -3 and b"workspace" in lib.fc_last_error()
-    rc = lib.fc_mask_encode(addr, 10, 99, None, 0.5, 0, 0, 1, None, addr, addr, 10, addr, addr,
-                            addr, 1 << 20, None)
+    rc = lib.fc_mask_encode(addr, 10, 99, None, 0.5, 0, 0, 1, None, addr, addr, 10, addr, None,
+                            addr, addr, 1 << 20, None)
     assert rc == -1 and b"bad codec" in lib.fc_last_error()
     with pytest.raises(_lib.FedCodecError):
         _lib.check(lib.fc_decode_accumulate(None, 1, 0, 10, None, None), "decode_accumulate")

@@ -38,10 +38,10 @@ def main():
     import numpy as np
     import torch
 
-    from openmsftl_amd import _lib as L
-    from openmsftl_amd import codec
     from openmsftl_amd.compression import kept_count
     from openmsftl_amd.distributed import fedavg_weights
+
+    from openmsftl_amd.pipeline import HostFedAvg
 
     dev = torch.device("cuda", 0)
     n, C, Gs, R = args.n, args.clients, args.group, args.ring
@@ -53,47 +53,13 @@ def main():
         g.mul_(10.0 ** np.random.default_rng(i).uniform(-4, -1))
         host.append(g.pin_memory())
     print(f"[e2e] host pool ready in {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
-    slots = [torch.empty(n, dtype=torch.float32, device=dev) for _ in range(R)]
-    hdrs = torch.empty((Gs, L.HDR_BYTES), dtype=torch.uint8, device=dev)
-    pkts = [codec.Packet.alloc(n, L.FC_FMT_IDXVAL, dev, hdr=hdrs[j], k=k) for j in range(Gs)]
+    pipe = HostFedAvg(n, k, group=Gs, ring=R, device=dev)
     w = fedavg_weights(C)
-    views = [codec.views_tensor(pkts, [float(x) for x in w[g0:g0 + Gs]], dev)
-             for g0 in range(0, C, Gs)]
-    acc = torch.empty(n, dtype=torch.float32, device=dev)
-    out_host = torch.empty(n, dtype=torch.float32).pin_memory()
-    scratch = torch.empty(n, dtype=torch.float32, device=dev)
-    comp = torch.cuda.current_stream(dev)
-    copy = torch.cuda.Stream(dev)
-    h2d_done = [torch.cuda.Event() for _ in range(R)]
-    enc_done = [torch.cuda.Event() for _ in range(R)]
-    for e in enc_done:
-        e.record(comp)
 
     def run():
-        redo = 0
-        for g0 in range(0, C, Gs):
-            m = min(Gs, C - g0)
-            for j in range(m):
-                i = g0 + j
-                s = i % R
-                copy.wait_event(enc_done[s])
-                with torch.cuda.stream(copy):
-                    slots[s].copy_(host[i % len(host)], non_blocking=True)
-                    h2d_done[s].record(copy)
-                comp.wait_event(h2d_done[s])
-                codec.encode_top(slots[s], k, packet=pkts[j], check=False)
-                enc_done[s].record(comp)
-            status = hdrs[:m, 36:40].cpu()            # one sync per group
-            if bool((status != 0).any()):             # exact re-encode from the host copy
-                for j in np.nonzero(status.numpy().view(np.uint32).ravel())[0]:
-                    scratch.copy_(host[(g0 + int(j)) % len(host)])
-                    codec.encode_top(scratch, k, packet=pkts[int(j)], exact=True)
-                    redo += 1
-            codec.decode_accumulate(pkts[:m], None, out=acc, views=views[g0 // Gs],
-                                    continue_sum=g0 > 0)
-        out_host.copy_(acc, non_blocking=True)
-        torch.cuda.synchronize()
-        return redo
+        before = pipe.exact_fallbacks
+        pipe.run(lambda i: host[i % len(host)], C, w)
+        return pipe.exact_fallbacks - before
 
     run()                                             # warm-up (allocations, code objects)
     times, redo = [], 0
@@ -114,7 +80,7 @@ def main():
     torch.cuda.synchronize()
     t = time.perf_counter()
     for i in range(8):
-        slots[0].copy_(host[i % len(host)], non_blocking=True)
+        pipe.slots[0].copy_(host[i % len(host)], non_blocking=True)
     torch.cuda.synchronize()
     line["h2d_alone_GBps"] = round(8 * 4.0 * n / (time.perf_counter() - t) / 1e9, 2)
     print(json.dumps(line), flush=True)

@@ -2,13 +2,17 @@
 
     python tools/rocpd_summary.py stats <results.db> <out_kernel_stats.csv>
     python tools/rocpd_summary.py pmc <fetch.db> <write.db> <kernel-substring> <out.json> \
-        [--alg-bytes B]
+        [--alg-bytes B] [--calib profiles/<tag>_pmc_calib.json]
+    python tools/rocpd_summary.py calib <fetch.db> <write.db> <out.json>
 
 `stats` is the per-kernel table rocprofv3 --stats prints (calls, total/avg/min/max ns, %).
 `pmc` averages FETCH_SIZE / WRITE_SIZE (kilobytes, one --pmc pass each) over the dispatches of
-one kernel and converts them to HBM bytes per launch the way MI355X_MICROARCH.md §HBM
-prescribes for gfx950: FETCH_SIZE reports half the bytes of a wide (16 B/lane) streaming read,
-so it is doubled; WRITE_SIZE is exact for 16 B/lane streaming stores.
+one kernel and converts them to HBM bytes per launch.  MI355X_MICROARCH.md §HBM: on gfx950
+FETCH_SIZE reports half the bytes of a wide (16 B/lane) streaming read and WRITE_SIZE is exact
+for 16 B/lane streaming stores; other widths must be calibrated on a known byte count.
+`calib` does that with tools/pmc_calib.hip's kernels (512 MiB each, k_compact_mag1's 4 B/lane
+non-temporal read and its store shapes) and `pmc --calib` applies the measured factors
+(read: k_read4_nt, write: k_write16) instead of the 16 B/lane defaults.
 """
 from __future__ import annotations
 
@@ -55,20 +59,47 @@ def pmc_values(db, counter, substr):
     return [float(v) for name, v in c.execute(q, (counter,)) if substr in name]
 
 
-def pmc(fetch_db, write_db, substr, out, alg_bytes=None, clients=1):
+CALIB_BYTES = 512 * 1024 * 1024          # tools/pmc_calib.py: bytes per calibration dispatch
+
+
+def calib(fetch_db, write_db, out):
+    """Bytes / reported bytes for each calibration kernel (its known 512 MiB)."""
+    res = {"known_bytes_per_dispatch": CALIB_BYTES, "source": "tools/pmc_calib.hip"}
+    for kern, db, ctr in (("k_read4_nt", fetch_db, "FETCH_SIZE"), ("k_read16", fetch_db, "FETCH_SIZE"),
+                          ("k_write16", write_db, "WRITE_SIZE"), ("k_write4_nt", write_db, "WRITE_SIZE")):
+        v = pmc_values(db, ctr, kern)
+        if not v:
+            raise SystemExit(f"no {ctr} for {kern}")
+        kb = statistics.mean(v)
+        res[kern] = {"counter": ctr, "dispatches": len(v), "reported_kb_avg": round(kb, 1),
+                     "factor": round(CALIB_BYTES / (kb * 1024.0), 4)}
+    with open(out, "w") as fh:
+        json.dump(res, fh, indent=1)
+    return res
+
+
+def pmc(fetch_db, write_db, substr, out, alg_bytes=None, clients=1, calib_path=None):
     f = pmc_values(fetch_db, "FETCH_SIZE", substr)
     w = pmc_values(write_db, "WRITE_SIZE", substr)
     if not f or not w:
         raise SystemExit(f"no dispatches of {substr!r} with FETCH_SIZE/WRITE_SIZE")
     fetch_kb, write_kb = statistics.mean(f), statistics.mean(w)
-    hbm = 2.0 * fetch_kb * 1024 + write_kb * 1024
+    rf, wf = 2.0, 1.0
+    corr = ("MI355X_MICROARCH.md §HBM: FETCH_SIZE x2 (gfx950 half-count of 16 B/lane streaming "
+            "reads); WRITE_SIZE as reported")
+    if calib_path:
+        cal = json.load(open(calib_path))
+        rf, wf = cal["k_read4_nt"]["factor"], cal["k_write16"]["factor"]
+        corr = (f"calibrated on known 512 MiB dispatches of the same access shapes ({calib_path}): "
+                f"FETCH_SIZE x {rf} (4 B/lane non-temporal reads), WRITE_SIZE x {wf} "
+                "(16 B/lane stores)")
+    hbm = rf * fetch_kb * 1024 + wf * write_kb * 1024
     res = {"kernel": substr, "dispatches_fetch": len(f), "dispatches_write": len(w),
            "fetch_size_kb_avg": round(fetch_kb, 1), "write_size_kb_avg": round(write_kb, 1),
-           "hbm_read_bytes_per_launch": int(2.0 * fetch_kb * 1024),
-           "hbm_write_bytes_per_launch": int(write_kb * 1024),
+           "hbm_read_bytes_per_launch": int(rf * fetch_kb * 1024),
+           "hbm_write_bytes_per_launch": int(wf * write_kb * 1024),
            "hbm_bytes_per_launch": int(hbm), "clients_per_launch": clients,
-           "correction": "MI355X_MICROARCH.md §HBM: FETCH_SIZE x2 (gfx950 half-count of "
-                         "16 B/lane streaming reads); WRITE_SIZE as reported"}
+           "correction": corr}
     if alg_bytes:
         res["alg_bytes_per_launch"] = int(alg_bytes)
         res["traffic_over_alg"] = round(hbm / alg_bytes, 4)
@@ -90,13 +121,20 @@ def main():
     p.add_argument("out")
     p.add_argument("--alg-bytes", type=float, default=None)
     p.add_argument("--clients-per-launch", type=int, default=1)
+    p.add_argument("--calib", default=None)
+    c = sub.add_parser("calib")
+    c.add_argument("fetch_db")
+    c.add_argument("write_db")
+    c.add_argument("out")
     a = ap.parse_args()
     if a.cmd == "stats":
         for name, d in stats(a.db, a.out)[:12]:
             print(f"{len(d):7d} {sum(d) / len(d) / 1e3:10.2f} us  {name[:100]}")
+    elif a.cmd == "calib":
+        print(json.dumps(calib(a.fetch_db, a.write_db, a.out), indent=1))
     else:
         print(json.dumps(pmc(a.fetch_db, a.write_db, a.kernel, a.out, a.alg_bytes,
-                             a.clients_per_launch), indent=1))
+                             a.clients_per_launch, a.calib), indent=1))
 
 
 if __name__ == "__main__":
