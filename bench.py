@@ -207,7 +207,11 @@ def main():
     jobs = codec.encode_jobs(grads, pkts)
     per_launch = 1 if args.no_batch else M          # clients per k_compact launch
     fedavg = ShardedFedAvg(mode="reduce", dst=0)
-    acc = torch.empty(n, dtype=torch.float32, device=device)
+    # two aggregate buffers: step i's RCCL reduce (async, on RCCL's stream) runs under step
+    # i+1's encodes; step i+2 waits for it before folding into the same buffer again
+    accs = [torch.empty(n, dtype=torch.float32, device=device) for _ in range(2)]
+    works = [None, None]
+    nstep = [0]
     redo_total = [0]
 
     def step():
@@ -220,8 +224,12 @@ def main():
         status = hdrs[:, 36:40].cpu()               # fc_packet_hdr.status (synchronises)
         if bool((status != 0).any()):               # sampled bracket missed: exact re-encode
             redo_total[0] += codec.resolve(pkts)
-        # local fold of this rank's shard (k_decode<ACC>) + RCCL fp32 reduce to rank 0
-        fedavg.aggregate(fold, M * world, acc, weights=w_all)
+        # local fold of this rank's shard (k_fold_q) + RCCL fp32 reduce to rank 0
+        b = nstep[0] & 1
+        nstep[0] += 1
+        if works[b] is not None:
+            works[b].wait()                         # stream-side wait for step i-2's reduce
+        works[b] = fedavg.aggregate(fold, M * world, accs[b], weights=w_all, async_op=True)
 
     for _ in range(args.warmup):
         step()

@@ -18,6 +18,14 @@ path, then combines the per-rank partial sums in one of two ways:
 
 The local fold is a callable so the same orchestration drives the HIP packets
 (:func:`packet_fold`) and, in the CPU tests, a plain sequential sum over gloo.
+
+Backends: with ``nccl`` (RCCL over xGMI) the device tensors travel directly; gloo has no
+device ``reduce``/``send``/``recv``, so for a device ``out`` on a gloo group the partial sums
+are staged through host memory (same bytes, same order of additions: the chain stays
+bit-exact; tests/test_distributed_gpu.py runs two gloo ranks on one GPU that way).
+``aggregate(..., async_op=True)`` (reduce mode, RCCL) returns the collective's work handle
+instead of waiting, so a caller with a second ``out`` buffer overlaps the reduce of step i
+with the encodes of step i+1 (bench.py does).
 """
 from __future__ import annotations
 
@@ -56,45 +64,79 @@ class ShardedFedAvg:
             raise ValueError(f"mode must be 'reduce' or 'chain' (got {mode!r})")
         self.mode, self.dst, self.group = mode, dst, group
 
+    def _staged(self, t) -> bool:
+        """gloo group + device tensor: communicate through a host copy."""
+        import torch.distributed as dist
+        return t.is_cuda and dist.get_backend(self.group) == "gloo"
+
+    def _reduce(self, out, async_op: bool):
+        import torch.distributed as dist
+        if self._staged(out):
+            h = out.cpu()
+            dist.reduce(h, dst=self.dst, op=dist.ReduceOp.SUM, group=self.group)
+            if dist.get_rank(self.group) == self.dst:
+                out.copy_(h)
+            return None
+        return dist.reduce(out, dst=self.dst, op=dist.ReduceOp.SUM, group=self.group,
+                           async_op=async_op)
+
+    def _send(self, out, dst: int):
+        import torch.distributed as dist
+        dist.send(out.cpu() if self._staged(out) else out, dst=dst, group=self.group)
+
+    def _recv(self, out, src: int):
+        import torch.distributed as dist
+        if self._staged(out):
+            h = _host_like(out)
+            dist.recv(h, src=src, group=self.group)
+            out.copy_(h)
+        else:
+            dist.recv(out, src=src, group=self.group)
+
     def _world(self):
         import torch.distributed as dist
         if not dist.is_available() or not dist.is_initialized():
             return 1, 0
         return dist.get_world_size(self.group), dist.get_rank(self.group)
 
-    def aggregate(self, local_fold: Fold, num_clients: int, out, weights=None):
+    def aggregate(self, local_fold: Fold, num_clients: int, out, weights=None,
+                  async_op: bool = False):
         """Fold this rank's shard into ``out`` and combine across ranks.  The complete
         aggregate is valid on ``dst`` only (``out`` elsewhere holds scratch).  ``weights``:
-        float32 per G row (default 1/M each, gar.py:37-40)."""
-        import torch.distributed as dist
+        float32 per G row (default 1/M each, gar.py:37-40).  ``async_op`` (reduce mode):
+        return the reduce's work handle (``None`` when there is nothing to wait for) and
+        leave ``out`` in flight until ``handle.wait()``."""
         world, rank = self._world()
         w = fedavg_weights(num_clients) if weights is None else np.asarray(weights, np.float32)
         if w.shape != (num_clients,):
             raise AssertionError("weights must have one entry per client")   # gar.py:41-42
         rows = shard_range(num_clients, world, rank)
         if world == 1:
-            return local_fold(rows, w[rows.start:rows.stop], out, False)
+            local_fold(rows, w[rows.start:rows.stop], out, False)
+            return None if async_op else out
         if self.mode == "reduce":
             if len(rows):
                 local_fold(rows, w[rows.start:rows.stop], out, False)
             else:
                 out.zero_()                      # empty shard adds nothing
-            dist.reduce(out, dst=self.dst, op=dist.ReduceOp.SUM, group=self.group)
-            return out
+            work = self._reduce(out, async_op)
+            return work if async_op else out
+        if async_op:
+            raise ValueError("async_op is for mode='reduce' (the chain is serial by design)")
         # chain: rank r continues rank r-1's left-to-right fold (bit-identical to 1 GPU)
         first = min(r for r in range(world) if len(shard_range(num_clients, world, r)))
         last = max(r for r in range(world) if len(shard_range(num_clients, world, r)))
         if len(rows):
             if rank != first:
-                dist.recv(out, src=self._prev(rank, num_clients, world), group=self.group)
+                self._recv(out, self._prev(rank, num_clients, world))
             local_fold(rows, w[rows.start:rows.stop], out, rank != first)
             if rank != last:
-                dist.send(out, dst=self._next(rank, num_clients, world), group=self.group)
+                self._send(out, self._next(rank, num_clients, world))
         if last != self.dst:
             if rank == last:
-                dist.send(out, dst=self.dst, group=self.group)
+                self._send(out, self.dst)
             elif rank == self.dst:
-                dist.recv(out, src=last, group=self.group)
+                self._recv(out, last)
         return out
 
     @staticmethod
@@ -104,6 +146,11 @@ class ShardedFedAvg:
     @staticmethod
     def _next(rank, m, world):
         return min(r for r in range(rank + 1, world) if len(shard_range(m, world, r)))
+
+
+def _host_like(t):
+    import torch
+    return torch.empty(t.shape, dtype=t.dtype)
 
 
 def packet_fold(packets, views=None) -> Fold:

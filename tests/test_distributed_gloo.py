@@ -46,13 +46,18 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, M, n, mode, dst, seed, q):
+def _worker(rank, world, port, M, n, mode, dst, seed, q, async_op=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         rows = _rows(M, n, seed)
         out = torch.empty(n, dtype=torch.float32)
-        ShardedFedAvg(mode=mode, dst=dst).aggregate(_oracle_fold(rows), M, out)
+        fa = ShardedFedAvg(mode=mode, dst=dst)
+        if async_op:                                      # bench.py's overlapped reduce
+            work = fa.aggregate(_oracle_fold(rows), M, out, async_op=True)
+            work.wait()
+        else:
+            fa.aggregate(_oracle_fold(rows), M, out)
         if rank == dst:
             q.put(out.numpy().copy())
         dist.barrier()
@@ -60,11 +65,11 @@ def _worker(rank, world, port, M, n, mode, dst, seed, q):
         dist.destroy_process_group()
 
 
-def _run(world, M, n, mode, dst=0, seed=0):
+def _run(world, M, n, mode, dst=0, seed=0, async_op=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, M, n, mode, dst, seed, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, M, n, mode, dst, seed, q, async_op))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -104,13 +109,13 @@ def test_chain_is_bit_exact(world, M):
     assert got.tobytes() == go.FedAvgOracle({}).aggregate(G).tobytes()   # gar.py:44 itself
 
 
-@pytest.mark.parametrize("world,M", [(2, 8), (3, 10)])
-def test_reduce_within_reassociation_bound(world, M):
+@pytest.mark.parametrize("world,M,async_op", [(2, 8, False), (3, 10, False), (2, 8, True)])
+def test_reduce_within_reassociation_bound(world, M, async_op):
     n = 4099
     rows = _rows(M, n, seed=1)
     w = fedavg_weights(M)
     ref = go.sequential_weighted_sum(rows, w)
-    got = _run(world, M, n, "reduce", seed=1)
+    got = _run(world, M, n, "reduce", seed=1, async_op=async_op)
     mag = np.sum(np.abs(np.stack(rows) * w[:, None]), axis=0, dtype=np.float64)
     tol = (M + world) * 2.0 ** -24 * mag                 # stated in distributed.py
     assert np.all(np.abs(got.astype(np.float64) - ref) <= tol)
