@@ -200,6 +200,26 @@ static int launch_compact_key(int key_mode, const CompactArgs& a, hipStream_t s)
   return FC_OK;
 }
 
+// k_fused_mag (sample + compaction in one launch) for a lone magnitude-key client;
+// FC_UNFUSED=1 selects the two-launch form (A/B only).
+static bool fused_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("FC_UNFUSED");
+    return !(e && atoi(e) != 0);
+  }();
+  return on;
+}
+
+static int launch_fused(const CompactArgs& ca, const SamplePlan& P, const HdrInit& hi,
+                         uint32_t nsamp, hipStream_t s) {
+  TimedLaunch t(FC_TIME_COMPACT, s);
+  const dim3 grid(nsamp + ca.nchunks);
+  if (ca.dense) hipLaunchKernelGGL(k_fused_mag<true>, grid, dim3(kCBlock), 0, s, ca, P, hi, nsamp);
+  else hipLaunchKernelGGL(k_fused_mag<false>, grid, dim3(kCBlock), 0, s, ca, P, hi, nsamp);
+  FC_LAUNCHED("k_fused_mag");
+  return FC_OK;
+}
+
 static int launch_resolve(const ResolveArgs& a, hipStream_t s) {
   TimedLaunch t(FC_TIME_ENGINE, s);
   const uint32_t grid = a.nchunks < (uint32_t)kResolveGrid ? a.nchunks : (uint32_t)kResolveGrid;
@@ -318,6 +338,11 @@ int fc_topk_encode(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_
   hipStream_t s = (hipStream_t)stream;
   const SamplePlan P = make_plan(n, k);
   const uint32_t sgrid = (P.nseg + kSampleSegs - 1) / kSampleSegs;   // <= 256
+  if (key_mode == FC_KEY_MAGNITUDE && fused_enabled()) {
+    rc = launch_fused(ca, P, hi, sgrid, s);
+    if (rc) return rc;
+    return launch_resolve(ra, s);
+  }
   rc = launch_sample(key_mode, dim3(sgrid), g, P, seed, offset, ca.W, ca.ib, hdr, hi, nullptr, 0ull, s);
   if (rc) return rc;
   rc = launch_compact_key(key_mode, ca, s);
@@ -339,9 +364,12 @@ int fc_topk_encode_dense(const float* g, uint64_t n, uint64_t k, uint32_t* idx, 
   hipStream_t s = (hipStream_t)stream;
   const SamplePlan P = make_plan(n, k);
   const uint32_t sgrid = (P.nseg + kSampleSegs - 1) / kSampleSegs;
-  rc = launch_sample(FC_KEY_MAGNITUDE, dim3(sgrid), g, P, 0ull, 0ull, ca.W, ca.ib, hdr, hi, nullptr, 0ull, s);
-  if (rc) return rc;
-  {
+  if (fused_enabled()) {
+    rc = launch_fused(ca, P, hi, sgrid, s);
+    if (rc) return rc;
+  } else {
+    rc = launch_sample(FC_KEY_MAGNITUDE, dim3(sgrid), g, P, 0ull, 0ull, ca.W, ca.ib, hdr, hi, nullptr, 0ull, s);
+    if (rc) return rc;
     TimedLaunch t(FC_TIME_COMPACT, s);
     hipLaunchKernelGGL(k_compact_mag1_dense, dim3(ca.nchunks, 1), dim3(kCBlock), 0, s, ca);
     FC_LAUNCHED("k_compact_mag1_dense");

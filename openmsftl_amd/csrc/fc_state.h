@@ -25,9 +25,9 @@ struct alignas(16) TopkState {
   uint32_t small_n;      // survivors gathered for the LDS finish
   uint32_t e_shift, e_rank, e_matched, e_done, e_ticket, e_status;
   uint32_t gen;          // k_resolve generation: bumped when T64 is published (dense fix-up)
-  uint32_t st_pub;       // status published with T_pub
-  uint64_t T_pub;        // T64 published to the waiting k_resolve workgroups
-  uint32_t pad_[2];
+  uint32_t fz_pub;       // k_fused_mag: the bracket is written (= fz_seq + 1 of that launch)
+  uint32_t fz_seq;       // k_fused_mag launches completed (bumped by the following k_resolve)
+  uint32_t pad_[3];
   uint32_t shard_ent[kShards];   // k_compact totals, 64-way sharded (no hot word)
   uint32_t shard_cnd[kShards];
 };

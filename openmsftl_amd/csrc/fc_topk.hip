@@ -169,11 +169,12 @@ __device__ __forceinline__ uint32_t fine_upper(uint32_t b, const FineWin& F) {
 }
 
 // Segment s of the sample: element range [e, lim) of this thread's float4.
-__device__ __forceinline__ void seg_lane(const SamplePlan& P, uint32_t s, int tid, uint64_t& e,
-                                         uint64_t& lim) {
+// (n < 2^32: 32-bit bounds keep k_fused_mag's sample part inside 64 VGPRs)
+__device__ __forceinline__ void seg_lane(const SamplePlan& P, uint32_t s, int tid, uint32_t& e,
+                                         uint32_t& lim) {
   const uint64_t st = seg_start(P, s);
-  lim = P.full ? (st + 1024 < P.n ? st + 1024 : P.n) : st + 1024;
-  e = st + (uint64_t)tid * 4;
+  lim = (uint32_t)(P.full ? (st + 1024 < P.n ? st + 1024 : P.n) : st + 1024);
+  e = (uint32_t)st + (uint32_t)tid * 4u;
 }
 
 // Pilot level-1 histogram (key >> 19) of the kPilotSegs pilot segments -> the window.
@@ -183,12 +184,12 @@ __device__ __forceinline__ FineWin pilot_window(const float* __restrict__ g, con
                                                 uint64_t seed, uint64_t off, uint32_t* h,
                                                 uint32_t* s_tmp, uint32_t* s_out, bool own,
                                                 const float4 (&xs)[kSampleSegs],
-                                                const uint64_t (&es)[kSampleSegs],
-                                                const uint64_t (&ls)[kSampleSegs]) {
+                                                const uint32_t (&es)[kSampleSegs],
+                                                const uint32_t (&ls)[kSampleSegs]) {
   static_assert(kPilotSegs == kSampleSegs, "the pilot is workgroup 0's share of the sample");
   const int tid = threadIdx.x;
   float4 xp[kPilotSegs];
-  uint64_t ep[kPilotSegs], lp[kPilotSegs];
+  uint32_t ep[kPilotSegs], lp[kPilotSegs];
 #pragma unroll
   for (int q = 0; q < kPilotSegs; ++q) {
     if (own) {
@@ -230,29 +231,33 @@ __device__ __forceinline__ FineWin pilot_window(const float* __restrict__ g, con
 // payload + flag; the others load their segments meanwhile): 256 workgroups re-reading the same
 // 32 KB pilot took ~7 us of loads.  A batched launch (too many workgroups to wait on each
 // other) has every workgroup compute the window itself.
+struct SampleShared {
+  uint32_t h[kHistBins];                          // pilot histogram, then the sample's
+  uint32_t s_tmp[8], s_out[4], s_flag, s_win[3];
+};
+
+// The body of k_sample1 for workgroup bid of nb (256 threads).  shared_pilot: a lone client's
+// launch (workgroup 0 publishes the window).  pub != 0 (k_fused_mag): once the bracket is
+// written, publish it to the compaction workgroups of the same launch (S->fz_pub = pub).
 template <int KM>
-__global__ __launch_bounds__(kBlock) void k_sample1(const float* __restrict__ g, SamplePlan P,
-                                                    uint64_t seed, uint64_t off, WsPtrs W,
-                                                    uint32_t ib, fc_packet_hdr* hdr, HdrInit HI,
-                                                    const fc_encode_job* jobs,
-                                                    uint64_t ws_stride) {
-  __shared__ uint32_t h[kHistBins];               // pilot histogram, then the sample's
-  __shared__ uint32_t s_tmp[8], s_out[4], s_flag, s_win[3];
-  if (jobs) {                                     // batched: client blockIdx.y
-    const fc_encode_job& J = jobs[blockIdx.y];
-    g = J.g; hdr = J.hdr; seed = J.seed; off = J.offset;
-    HI.seed = seed; HI.offset = off;
-    W = ws_shift(W, (uint64_t)blockIdx.y * ws_stride);
-  }
+__device__ __forceinline__ void sample_body(const float* __restrict__ g, const SamplePlan& P,
+                                            uint64_t seed, uint64_t off, const WsPtrs& W,
+                                            uint32_t ib, fc_packet_hdr* hdr, const HdrInit& HI,
+                                            uint32_t bid, uint32_t nb, bool shared_pilot,
+                                            SampleShared& sm, uint32_t pub) {
+  uint32_t* h = sm.h;
+  uint32_t* s_tmp = sm.s_tmp;
+  uint32_t* s_out = sm.s_out;
+  uint32_t* s_win = sm.s_win;
   TopkState* S = W.st;
   const int tid = threadIdx.x;
   FC_TR(0);
   // this workgroup's segments first (plain loads: ~2 us sooner than non-temporal here)
   float4 xs[kSampleSegs];
-  uint64_t es[kSampleSegs], ls[kSampleSegs];
+  uint32_t es[kSampleSegs], ls[kSampleSegs];
 #pragma unroll
   for (int q = 0; q < kSampleSegs; ++q) {
-    const uint32_t s = blockIdx.x + (uint32_t)q * gridDim.x;
+    const uint32_t s = bid + (uint32_t)q * nb;
     es[q] = ls[q] = 0;
     xs[q] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (s < P.nseg) {
@@ -261,11 +266,10 @@ __global__ __launch_bounds__(kBlock) void k_sample1(const float* __restrict__ g,
     }
   }
   for (int b = tid; b < kHistBins; b += kBlock) h[b] = 0;
-  if (blockIdx.x == 0 && tid == 0) write_hdr_static(hdr, HI);
-  const bool shared_pilot = gridDim.y == 1;       // uniform
+  if (bid == 0 && tid == 0) write_hdr_static(hdr, HI);
   FineWin F;
-  if (!shared_pilot || blockIdx.x == 0) {
-    F = pilot_window<KM>(g, P, seed, off, h, s_tmp, s_out, blockIdx.x == 0, xs, es, ls);
+  if (!shared_pilot || bid == 0) {
+    F = pilot_window<KM>(g, P, seed, off, h, s_tmp, s_out, bid == 0, xs, es, ls);
     if (shared_pilot && tid == 0) {               // publish: sc1 payload, drained, sc1 flag
       st_agent(&S->win_klo, F.klo); st_agent(&S->win_khi, F.khi); st_agent(&S->win_fs, F.fs);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -301,12 +305,12 @@ __global__ __launch_bounds__(kBlock) void k_sample1(const float* __restrict__ g,
   __syncthreads();
   FC_TR(3);
   {                                               // flush into this workgroup's shard
-    uint32_t* gh = W.hist1 + (blockIdx.x % kSampleShards) * kHistBins;
+    uint32_t* gh = W.hist1 + (bid % kSampleShards) * kHistBins;
     for (int b = tid; b < kHistBins; b += kBlock)
       if (h[b]) atomicAdd(&gh[b], h[b]);
   }
   FC_TR(4);
-  if (!last_block_arrive_tree(W.tick, gridDim.x, blockIdx.x, &s_flag, 18)) return;
+  if (!last_block_arrive_tree(W.tick, nb, bid, &sm.s_flag, 18)) return;
   FC_TR(5);
   // ---- last workgroup: the bracket (read + clear the histogram) ----
   {
@@ -327,22 +331,46 @@ __global__ __launch_bounds__(kBlock) void k_sample1(const float* __restrict__ g,
   find_ranks_desc(h, P.hi_none ? 1u : (uint32_t)P.r_hi, P.lo_all ? 1u : (uint32_t)P.r_lo, s_tmp, s_out);
   const uint32_t t_hi = P.hi_none ? 0xffffffffu : fine_upper(s_out[0], F);
   const uint32_t t_lo = P.lo_all ? 0u : fine_lower(s_out[2], F);
-  if (tid < kShards) { S->shard_ent[tid] = 0; S->shard_cnd[tid] = 0; }  // k_compact totals
+  // the state k_compact reads; sc1 stores from wave 0 so that a publication (pub) after its
+  // drain makes them visible to the compaction workgroups of the same launch on every XCD
+  if (tid < kShards) { st_agent(&S->shard_ent[tid], 0u); st_agent(&S->shard_cnd[tid], 0u); }
   if (tid == 0) {
     const uint64_t span = (uint64_t)t_hi - t_lo;          // candidate keys: [t_lo, t_hi]
     uint32_t sb = 0;
     while ((span >> sb) >= (uint64_t)kHistBins) ++sb;
-    S->t_lo = t_lo; S->t_hi = t_hi; S->sbin = sb; S->L64 = (uint64_t)t_lo << ib;
-    S->cand_on = 1; S->n_cand = 0; S->cand_over = 0; S->ent_over = 0;
+    st_agent(&S->t_lo, t_lo); st_agent(&S->t_hi, t_hi); st_agent(&S->sbin, sb);
+    st_agent(&S->L64, (uint64_t)t_lo << ib);
+    st_agent(&S->cand_on, 1u);
+    S->n_cand = 0; S->cand_over = 0; S->ent_over = 0;
     S->win_flag = 0;               // (err: set by a timed-out wait, read and
                                                   // cleared by this call's k_resolve)
     hdr->lower = (uint64_t)t_lo << ib;
+    if (pub) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      st_agent(&S->fz_pub, pub);
+    }
   }
   // clear the shards for the next call last, with plain 16-B stores (their next use is an
   // atomic in the next launch, after this kernel's end-of-launch write-back)
   for (int i = tid; i < kHistBins * kSampleShards / 4; i += kBlock)
     reinterpret_cast<uint4*>(W.hist1)[i] = make_uint4(0u, 0u, 0u, 0u);
   FC_TR(6);
+}
+
+template <int KM>
+__global__ __launch_bounds__(kBlock) void k_sample1(const float* __restrict__ g, SamplePlan P,
+                                                    uint64_t seed, uint64_t off, WsPtrs W,
+                                                    uint32_t ib, fc_packet_hdr* hdr, HdrInit HI,
+                                                    const fc_encode_job* jobs,
+                                                    uint64_t ws_stride) {
+  __shared__ SampleShared sm;
+  if (jobs) {                                     // batched: client blockIdx.y
+    const fc_encode_job& J = jobs[blockIdx.y];
+    g = J.g; hdr = J.hdr; seed = J.seed; off = J.offset;
+    HI.seed = seed; HI.offset = off;
+    W = ws_shift(W, (uint64_t)blockIdx.y * ws_stride);
+  }
+  sample_body<KM>(g, P, seed, off, W, ib, hdr, HI, blockIdx.x, gridDim.x, gridDim.y == 1, sm, 0u);
 }
 
 
@@ -1069,6 +1097,59 @@ __global__ __launch_bounds__(kCBlock, FC_MAG1_WAVES_PER_EU) void k_compact_mag1_
 // with spills at 80-96: DESIGN.md §Lessons.)
 
 // --------------------------------------------------------------------------------------
+// k_fused_mag: a lone client's k_sample1 + k_compact_mag1(_dense) in ONE launch.
+// Workgroups [0, nsamp) run the sample (256 of their 512 threads) and are dispatched first
+// (workgroups leave the dispatcher in order); every other workgroup is one chunk.  A chunk's
+// workgroup issues its loads, then waits (bounded relaxed sc1 poll) until the sample's last
+// workgroup publishes the bracket (S->fz_pub == fz_seq + 1, after its sc1 state stores have
+// drained), so the first resident round of chunk loads overlaps the sample's latency chain
+// instead of following it in a second launch.  fz_seq only changes in the k_resolve that
+// follows (stream order): every workgroup of this launch reads the same value.  The sample
+// never waits on a chunk workgroup, so no wait can deadlock; a timed-out one (never expected)
+// sets S->err, and the resolve reports RETRY (the caller re-encodes exactly).
+// --------------------------------------------------------------------------------------
+union FusedShared {
+  SampleShared s;
+  MagShared m;
+};
+
+template <bool DENSE>
+__global__ __launch_bounds__(kCBlock, FC_MAG1_WAVES_PER_EU) void k_fused_mag(CompactArgs a0, SamplePlan P,
+                                                                              HdrInit HI, uint32_t nsamp) {
+  __shared__ __attribute__((aligned(16))) FusedShared u;
+  __shared__ MagState s_st;
+  TopkState* S = a0.W.st;
+  const uint32_t pub = sload2(&S->fz_seq).x + 1u;   // not written by this launch
+  if (blockIdx.x < nsamp) {
+    if (threadIdx.x >= kBlock) return;
+    sample_body<kKeyMag>(a0.g, P, 0ull, 0ull, a0.W, a0.ib, a0.hdr, HI, blockIdx.x, nsamp, true, u.s, pub);
+    return;
+  }
+  const uint32_t chunk = blockIdx.x - nsamp;
+  float x[MagGeo<8>::kQ];
+  mag_load<8>(a0.g, chunk, a0.n, x);
+  FC_TR(24);
+  if (threadIdx.x == 0) {
+    uint32_t it = 0;
+    while (ld_agent(&S->fz_pub) != pub && ++it < kSpinMax) __builtin_amdgcn_s_sleep(4);
+    if (it >= kSpinMax) st_agent(&S->err, 1u);
+    MagState m;
+    m.L64 = ld_agent(&S->L64);
+    m.t_lo = ld_agent(&S->t_lo); m.t_hi = ld_agent(&S->t_hi);
+    m.cand_on = ld_agent(&S->cand_on); m.sbin = ld_agent(&S->sbin);
+    s_st = m;
+    u.m.ncand[0] = 0;
+  }
+  __syncthreads();
+  FC_TR(25);
+  const MagState st = s_st;
+  compact_mag_item<8, MagShared, DENSE>(a0, mag_out(a0, 0u), chunk, st, x, u.m, 0u);
+  FC_TR(26);
+}
+template __global__ void k_fused_mag<false>(CompactArgs, SamplePlan, HdrInit, uint32_t);
+template __global__ void k_fused_mag<true>(CompactArgs, SamplePlan, HdrInit, uint32_t);
+
+// --------------------------------------------------------------------------------------
 // k_resolve: exact T64 from the bracket's candidates (fast path, one launch).
 //   totals from the sharded counters -> rank r = k - #(key > t_hi) -> histogram bin beta
 //   holding rank r -> every workgroup gathers its chunks' candidates that fall in beta
@@ -1298,6 +1379,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve(ResolveArgs a0) {
     a.hdr->n_definite = n_hi;
     a.hdr->n_cand = n_cand;
     S->small_n = 0; S->err = 0;
+    S->fz_seq += 1u;               // k_fused_mag: the next launch publishes fz_seq + 1
   }
   FC_TR(15);
 }

@@ -43,9 +43,13 @@ def main():
     L.check(lib.fc_trace_read(buf.ctypes.data, buf.size), "trace")
     t = buf.reshape(-1, 32).astype(np.float64) / 100.0      # 100 MHz -> us
     res = {}
-    for name, slots in (("sample", [0, 20, 21, 22, 2, 3, 4, 18, 19, 5, 6]), ("resolve", [8, 9, 10, 11, 16, 17, 12, 13, 14, 15])):
+    # "fused": k_fused_mag's chunk workgroups (24 loads issued, 25 bracket received, 26 done),
+    # on the sample's clock (same launch)
+    for name, slots in (("sample", [0, 20, 21, 22, 2, 3, 4, 18, 19, 5, 6]), ("fused", [24, 25, 26]),
+                        ("resolve", [8, 9, 10, 11, 16, 17, 12, 13, 14, 15])):
         rec = t[:, slots[0]] > 0
-        t0 = t[rec, slots[0]].min() if rec.any() else 0.0
+        if name != "fused":
+            t0 = t[rec, slots[0]].min() if rec.any() else 0.0
         res[name] = {}
         for sl in slots:
             col = t[:, sl]
