@@ -13,7 +13,7 @@ aggregate to rank 0.  Weak scaling: per-GPU work is fixed.
 
 Prints ONE JSON line on rank 0.  `value` = gradient bytes (4 N per client, all ranks) per
 second of step time; `roofline` = the encode pass k_compact_mag1 (the dominant kernel), algorithmic
-bytes 4N + 8k per client over its HIP-event-timed average launch duration, `traffic` from the
+bytes 4N + 6k per client (ABI 3 packets: 6 B per entry) over its HIP-event-timed average launch duration, `traffic` from the
 committed calibrated PMC summary; `cpu_baseline` = the reference's exact NumPy calls
 (compression.py:31-37, default argsort) on one 128 M gradient, with every BASELINE.md §3 row
 in `extra.cpu_baseline_matrix`.  A self-check outside the timed region re-encodes two clients
@@ -32,6 +32,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+ENTRY_BYTES = 6.0             # packet entry: uint16 chunk-local index + fp32 value (ABI 3)
 
 
 def parse():
@@ -270,8 +271,9 @@ def main():
                                        streams=1)
             torch.cuda.synchronize()
     t_compact_us = kt_roof.avg_us("compact")
-    # the encode pass reads 4N and writes 8k per client
-    alg_bytes = per_launch * (4.0 * n + 8.0 * k)
+    # the encode pass reads 4N and writes the k entries per client, 6 B each in
+    # the ABI-3 packet (uint16 chunk-local index + fp32 value; §8(d) priced 8 B with uint32)
+    alg_bytes = per_launch * (4.0 * n + ENTRY_BYTES * k)
     achieved = alg_bytes / (t_compact_us * 1e-6) / 1e9
     pmc, pmc_src = load_pmc(args.pmc)
     roofline = {"kernel": "fc::k_compact_mag1 (top-k encode pass, %d client(s) per launch)"
@@ -292,8 +294,9 @@ def main():
                          if args.streams > 1 and not args.no_batch else "timed steps")
 
     # whole step against the HBM roofline (SURVEY §8(d) batched FedAvg with fused
-    # decode-accumulate: M (4N + 16k) + 4N algorithmic bytes per GPU and step)
-    step_alg = M * (4.0 * n + 16.0 * k) + 4.0 * n
+    # decode-accumulate: M (4N + 2 e k) + 4N algorithmic bytes per GPU and step, e = 6 B
+    # per packet entry)
+    step_alg = M * (4.0 * n + 2 * ENTRY_BYTES * k) + 4.0 * n
     step_gbps = step_alg * world / (elapsed / args.steps) / 1e9
     extra = {"per_step_kernel_time": breakdown, "exact_fallbacks": redo_total[0],
              "step_roofline": {"alg_bytes_per_gpu": int(step_alg),
@@ -341,7 +344,7 @@ def main():
 
 def single_gradient(torch, codec, g, k, n, iters=20):
     """North-star probe: encode+decode of ONE 128 M gradient (packet -> dense), HBM fraction
-    of the algorithmic 8N + 16k bytes."""
+    of the algorithmic 8N + 12k bytes (SURVEY §8(d) with 6-B packet entries)."""
     out = torch.empty_like(g)
     pkt = codec.encode_top(g, k)
     for _ in range(3):
@@ -365,7 +368,7 @@ def single_gradient(torch, codec, g, k, n, iters=20):
     torch.cuda.synchronize()
     dt_d = (time.perf_counter() - t0) / iters
     codec.resolve([pkt])
-    alg = 8.0 * n + 16.0 * k
+    alg = 8.0 * n + 2 * ENTRY_BYTES * k
     return {"n": n, "k": k, "us_per_encode_decode": round(dt * 1e6, 1),
             "grad_GBps": round(4.0 * n / dt / 1e9, 1),
             "alg_GBps": round(alg / dt / 1e9, 1),
@@ -401,7 +404,7 @@ def small_configs(torch, codec, L, device, f, n=16_777_216, M=128, steps=5):
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps
     redo = codec.resolve(pkts)
-    alg = M * (4.0 * n + 16.0 * k) + 4.0 * n
+    alg = M * (4.0 * n + 2 * ENTRY_BYTES * k) + 4.0 * n
     return {"config1_single_16M": one,
             "config2_128x16M": {"clients": M, "n": n, "k": k, "ms_per_step": round(dt * 1e3, 3),
                                 "grad_GBps": round(4.0 * n * M / dt / 1e9, 1),

@@ -37,7 +37,7 @@ extern "C" {
 
 typedef void* fc_stream_t; /* hipStream_t */
 
-#define FC_ABI_VERSION 2
+#define FC_ABI_VERSION 3
 
 /* return codes */
 #define FC_OK 0
@@ -63,13 +63,14 @@ typedef void* fc_stream_t; /* hipStream_t */
 #define FC_KEY_PHILOX 1      /* Philox4x32-10 word per element (native rand-k) */
 
 /* packet formats */
-#define FC_FMT_IDXVAL 0      /* uint32 idx[] ascending + float val[] */
+#define FC_FMT_IDXVAL 0      /* uint16 idx[] (chunk-local, ascending) + float val[] */
 #define FC_FMT_BITMAP 1      /* uint32 bitmap[ceil(N/8192)*256] + float val[] */
 #define FC_FMT_QSGD 2        /* packed W-bit codes (sign | level), fc_qsgd_code_words */
 
 /* Slotted packet layout: the gradient is cut into chunks of FC_CHUNK elements; chunk c's
  * entries (ascending index order) live at [c*FC_CHUNK, c*FC_CHUNK + cnt[c]) of idx/val (and
- * its bitmap words at [c*256, c*256+256)).  Every chunk is encoded by an independent
+ * its bitmap words at [c*256, c*256+256)).  idx holds the CHUNK-LOCAL index (uint16, the
+ * element is c*FC_CHUNK + idx): 6 bytes per entry instead of 8 (ABI 3).  Every chunk is encoded by an independent
  * workgroup — no global scan — so buffers are sized fc_packet_capacity(n) entries while only
  * the listed entries are written or read.
  * FC_FMT_IDXVAL packets also carry qoff[c] (uint64 per chunk): the slot positions where the
@@ -81,7 +82,7 @@ typedef void* fc_stream_t; /* hipStream_t */
 
 /* Device-resident packet header (96 bytes). */
 typedef struct fc_packet_hdr {
-  uint64_t thresh;      /* T64: entry kept iff (key<<index_bits | idx) >= thresh      */
+  uint64_t thresh;      /* T64: entry kept iff (key<<index_bits | index) >= thresh    */
   uint64_t lower;       /* L64: every element with comp >= lower is listed             */
   uint32_t n;           /* gradient length                                             */
   uint32_t k;           /* coordinates kept by the codec (top/rand)                    */
@@ -102,7 +103,7 @@ typedef struct fc_packet_hdr {
 
 /* One packet as seen by the decoders (host- or device-resident array element, 56 bytes). */
 typedef struct fc_packet_view {
-  const uint32_t* idx;          /* FC_FMT_IDXVAL                        */
+  const void* idx;              /* FC_FMT_IDXVAL: uint16 chunk-local indices; FC_FMT_QSGD: uint32 codes */
   const float* val;
   const uint32_t* bitmap;       /* FC_FMT_BITMAP                        */
   const uint32_t* cnt;          /* ceil(N/FC_CHUNK) entries per chunk   */
@@ -131,7 +132,7 @@ int fc_workspace_init(void* ws, size_t ws_bytes, fc_stream_t stream);
  * arguments.  capacity >= fc_packet_capacity(n); cnt and qoff have fc_num_chunks(n) words
  * (qoff may be NULL: not written, and the packet cannot be folded by fc_decode_accumulate). */
 int fc_topk_encode(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_t seed,
-                   uint64_t offset, uint32_t* idx, float* val, uint64_t capacity,
+                   uint64_t offset, uint16_t* idx, float* val, uint64_t capacity,
                    uint32_t* cnt, uint64_t* qoff, fc_packet_hdr* hdr, void* ws, size_t ws_bytes,
                    fc_stream_t stream);
 /* ---- top-k straight to the dense result (compression.py:31-37 returns q, not a packet) --
@@ -140,7 +141,7 @@ int fc_topk_encode(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_
  * launch zeroes the slack entries once T64 is known.  The packet is written as usual.  If the
  * header reports FC_STATUS_RETRY_EXACT, `dense` is not valid: re-encode with
  * fc_topk_encode_exact and fc_decode_dense (as for a packet).  Needs 0 < k < n. */
-int fc_topk_encode_dense(const float* g, uint64_t n, uint64_t k, uint32_t* idx, float* val,
+int fc_topk_encode_dense(const float* g, uint64_t n, uint64_t k, uint16_t* idx, float* val,
                          uint64_t capacity, uint32_t* cnt, uint64_t* qoff, fc_packet_hdr* hdr,
                          void* ws, size_t ws_bytes, float* dense, fc_stream_t stream);
 /* ---- batched top-k / native rand-k: M clients, one launch per pipeline stage ----------
@@ -152,7 +153,7 @@ int fc_topk_encode_dense(const float* g, uint64_t n, uint64_t k, uint32_t* idx, 
  * reports FC_STATUS_RETRY_EXACT is re-encoded with fc_topk_encode_exact, as for one client. */
 typedef struct fc_encode_job {
   const float* g;        /* gradient, 16-B aligned                          */
-  uint32_t* idx;         /* packet buffers (capacity >= fc_packet_capacity) */
+  uint16_t* idx;         /* packet buffers (capacity >= fc_packet_capacity) */
   float* val;
   uint32_t* cnt;
   fc_packet_hdr* hdr;
@@ -167,7 +168,7 @@ int fc_topk_encode_batch(const fc_encode_job* jobs_dev, int m, uint64_t n, uint6
 
 /* Exact radix-select path (several reads of g); always succeeds; n_entries == k. */
 int fc_topk_encode_exact(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_t seed,
-                         uint64_t offset, uint32_t* idx, float* val, uint64_t capacity,
+                         uint64_t offset, uint16_t* idx, float* val, uint64_t capacity,
                          uint32_t* cnt, uint64_t* qoff, fc_packet_hdr* hdr, void* ws,
                          size_t ws_bytes, fc_stream_t stream);
 
@@ -178,7 +179,7 @@ int fc_topk_encode_exact(const float* g, uint64_t n, uint64_t k, int key_mode, u
  * format: FC_FMT_BITMAP (bitmap required) or FC_FMT_IDXVAL (idx required; qoff written when
  * non-NULL). */
 int fc_mask_encode(const float* g, uint64_t n, int codec, const uint32_t* mask_bits,
-                   double p, uint64_t seed, uint64_t offset, int format, uint32_t* idx,
+                   double p, uint64_t seed, uint64_t offset, int format, uint16_t* idx,
                    float* val, uint32_t* bitmap, uint64_t capacity, uint32_t* cnt,
                    uint64_t* qoff, fc_packet_hdr* hdr, void* ws, size_t ws_bytes,
                    fc_stream_t stream);

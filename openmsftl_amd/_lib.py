@@ -151,7 +151,7 @@ def load(path: str = LIB_PATH):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        if lib.fc_abi_version() != 2:
+        if lib.fc_abi_version() != 3:
             raise FedCodecUnavailable("libfedcodec.so ABI mismatch")
         _lib = lib
         return lib

@@ -8,7 +8,8 @@
 
 Packets live on the GPU in the slotted layout of include/fedcodec.h: chunk c (8192 elements)
 lists its entries, ascending, at ``[c*8192, c*8192 + cnt[c])`` of ``idx``/``val`` (or
-``bitmap``/``val``); plus a 96-byte device header (``fc_packet_hdr``).
+``bitmap``/``val``); ``idx`` holds the chunk-local index as uint16 (element c*8192 + idx).
+Plus per-chunk counts and quarter offsets and a 96-byte device header (``fc_packet_hdr``).
 """
 from __future__ import annotations
 
@@ -22,6 +23,7 @@ import torch
 from . import _lib as L
 
 _U32 = torch.int32  # uint32 payloads are stored in int32 tensors (bit-identical)
+_U16 = torch.int16  # uint16 chunk-local indices in int16 tensors (bit-identical)
 
 
 def _vp(t: Optional[torch.Tensor]):
@@ -92,7 +94,7 @@ class Packet:
                    cnt=torch.empty(nch, dtype=_U32, device=device),
                    hdr=hdr if hdr is not None else torch.empty(L.HDR_BYTES, dtype=torch.uint8,
                                                                device=device),
-                   idx=torch.empty(cap, dtype=_U32, device=device) if fmt == L.FC_FMT_IDXVAL else None,
+                   idx=torch.empty(cap, dtype=_U16, device=device) if fmt == L.FC_FMT_IDXVAL else None,
                    bitmap=torch.empty(nch * 256, dtype=_U32, device=device)
                    if fmt == L.FC_FMT_BITMAP else None,
                    qoff=torch.empty(nch, dtype=torch.int64, device=device)
@@ -121,15 +123,17 @@ class Packet:
         return L.PacketHdr.from_buffer_copy(raw)
 
     def raw_entries(self):
-        """(idx uint32, val float32, header) of every LISTED entry, ascending — includes the
-        sampled-bracket slack (comp < thresh); inspection / test helper (synchronises)."""
+        """(idx uint32 = global element index, val float32, header) of every LISTED entry,
+        ascending — includes the sampled-bracket slack (comp < thresh); inspection / test
+        helper (synchronises)."""
         h = self.header()
         cnt = self.cnt.cpu().numpy().astype(np.int64)
         pos = np.arange(self.capacity, dtype=np.int64)
         listed = (pos % L.FC_CHUNK) < cnt[pos // L.FC_CHUNK]
         val = self.val.cpu().numpy()[listed]
         if self.fmt == L.FC_FMT_IDXVAL:
-            idx = self.idx.cpu().numpy().view(np.uint32)[listed]
+            local = self.idx.cpu().numpy().view(np.uint16)[listed].astype(np.uint32)
+            idx = (pos[listed] // L.FC_CHUNK * L.FC_CHUNK).astype(np.uint32) + local
         else:
             bits = np.unpackbits(self.bitmap.cpu().numpy().view(np.uint8), bitorder="little")
             idx = np.nonzero(bits[: self.n])[0].astype(np.uint32)

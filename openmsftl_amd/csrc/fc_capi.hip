@@ -278,7 +278,7 @@ int fc_workspace_init(void* ws, size_t ws_bytes, fc_stream_t stream) {
 }
 
 static int topk_args(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_t seed,
-                     uint64_t offset, uint32_t* idx, float* val, uint64_t capacity,
+                     uint64_t offset, uint16_t* idx, float* val, uint64_t capacity,
                      uint32_t* cnt, uint64_t* qoff, fc_packet_hdr* hdr, void* ws,
                      size_t ws_bytes, CompactArgs* ca, EngineArgs* ea, ResolveArgs* ra,
                      HdrInit* hi) {
@@ -311,7 +311,7 @@ static int topk_args(const float* g, uint64_t n, uint64_t k, int key_mode, uint6
 }
 
 int fc_topk_encode_exact(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_t seed,
-                         uint64_t offset, uint32_t* idx, float* val, uint64_t capacity,
+                         uint64_t offset, uint16_t* idx, float* val, uint64_t capacity,
                          uint32_t* cnt, uint64_t* qoff, fc_packet_hdr* hdr, void* ws,
                          size_t ws_bytes, fc_stream_t stream) {
   CompactArgs ca; EngineArgs ea; ResolveArgs ra; HdrInit hi;
@@ -325,7 +325,7 @@ int fc_topk_encode_exact(const float* g, uint64_t n, uint64_t k, int key_mode, u
 }
 
 int fc_topk_encode(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_t seed,
-                   uint64_t offset, uint32_t* idx, float* val, uint64_t capacity,
+                   uint64_t offset, uint16_t* idx, float* val, uint64_t capacity,
                    uint32_t* cnt, uint64_t* qoff, fc_packet_hdr* hdr, void* ws,
                    size_t ws_bytes, fc_stream_t stream) {
   if (k == 0 || k >= n)  // trivial thresholds: the exact engine resolves them in its init
@@ -350,7 +350,7 @@ int fc_topk_encode(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_
   return launch_resolve(ra, s);
 }
 
-int fc_topk_encode_dense(const float* g, uint64_t n, uint64_t k, uint32_t* idx, float* val,
+int fc_topk_encode_dense(const float* g, uint64_t n, uint64_t k, uint16_t* idx, float* val,
                          uint64_t capacity, uint32_t* cnt, uint64_t* qoff, fc_packet_hdr* hdr,
                          void* ws, size_t ws_bytes, float* dense, fc_stream_t stream) {
   FC_CHECK(dense != nullptr, "dense is NULL");
@@ -438,7 +438,7 @@ int fc_topk_encode_batch(const fc_encode_job* jobs, int m, uint64_t n, uint64_t 
 }
 
 int fc_mask_encode(const float* g, uint64_t n, int codec, const uint32_t* mask_bits, double p,
-                   uint64_t seed, uint64_t offset, int format, uint32_t* idx, float* val,
+                   uint64_t seed, uint64_t offset, int format, uint16_t* idx, float* val,
                    uint32_t* bitmap, uint64_t capacity, uint32_t* cnt, uint64_t* qoff,
                    fc_packet_hdr* hdr, void* ws, size_t ws_bytes, fc_stream_t stream) {
   int rc = check_common(g, n, ws, ws_bytes);

@@ -19,7 +19,7 @@
 namespace fc {
 
 struct PktCache {
-  const uint32_t* idx;
+  const void* idx;          // uint16 chunk-local indices (FC_FMT_IDXVAL)
   const float* val;
   const uint32_t* bitmap;
   const uint32_t* cnt;
@@ -104,10 +104,11 @@ constexpr int kDecBlocksPerCU = 4;
 // casts are plain global loads with a scalar base.
 typedef __attribute__((address_space(1))) const float gf32;
 typedef __attribute__((address_space(1))) const uint32_t gu32;
+typedef __attribute__((address_space(1))) const uint16_t gu16;   // chunk-local packet indices
 
 // Per-packet record staged in LDS once per workgroup (no per-step header/view loads).
 struct DecMeta {
-  const uint32_t* idx;        // FC_FMT_IDXVAL: idx; FC_FMT_BITMAP: bitmap
+  const void* idx;            // FC_FMT_IDXVAL: uint16 idx; FC_FMT_BITMAP: uint32 bitmap
   const float* val;
   const uint32_t* cnt;
   uint64_t seed, offset;      // rand-k (PHILOX) keys for the slack filter
@@ -153,20 +154,20 @@ template <int FMT>
 __device__ __forceinline__ void dec_load(DecItem& it, const DecMeta& pm, uint32_t c, int tid) {
   const uint64_t lo = (uint64_t)c * kChunk;
   gf32* val = (gf32*)pm.val + lo;                 // chunk slot base (scalar)
-  gu32* idx = (gu32*)pm.idx + lo;
+  gu16* idx = (gu16*)pm.idx + lo;
   it.cnt = ((gu32*)pm.cnt)[c];
 #pragma unroll
   for (int r = 0; r < kDecR; ++r) {
     const uint32_t e = (uint32_t)(tid + r * kDBlock);
     it.v[r] = val[e];
-    if (FMT == FC_FMT_IDXVAL) it.id[r] = idx[e];
+    if (FMT == FC_FMT_IDXVAL) it.id[r] = idx[e];                 // chunk-local
   }
   if (FMT == FC_FMT_BITMAP) it.bw = ((gu32*)pm.idx + (uint64_t)c * kChunkWords)[tid];
 }
 
 __device__ __forceinline__ PktCache meta_pkt(const DecMeta& pm) {
   PktCache c;
-  c.idx = pm.idx; c.val = pm.val; c.bitmap = pm.idx; c.cnt = pm.cnt; c.w = pm.w;
+  c.idx = pm.idx; c.val = pm.val; c.bitmap = (const uint32_t*)pm.idx; c.cnt = pm.cnt; c.w = pm.w;
   c.thresh = pm.thresh;
   c.ib = pm.flags & 0xffu; c.codec = (pm.flags >> 8) & 0xffu; c.key_mode = pm.flags >> 16;
   c.seed = pm.seed; c.offset = pm.offset; c.p = pm.p;
@@ -249,8 +250,8 @@ __global__ __launch_bounds__(kDBlock, kDecBlocksPerCU) void k_decode(DecodeArgs 
           if ((pk.key_mode == FC_KEY_PHILOX && pk.thresh != 0) || scale) {
             for (int r = 0; r < kDecR; ++r) {          // rand-k slack filter / scaling: one
               const uint32_t e = (uint32_t)(tid + r * kDBlock);   // entry at a time (VGPRs)
-              const uint32_t loc = cur.id[r] - (uint32_t)base;
-              if (e < cntv && loc < (uint32_t)kChunk && entry_kept(pk, cur.id[r], cur.v[r])) {
+              const uint32_t loc = cur.id[r];
+              if (e < cntv && loc < (uint32_t)kChunk && entry_kept(pk, (uint32_t)base + loc, cur.v[r])) {
                 tile[loc] = scale ? (float)((double)cur.v[r] / pk.p) : cur.v[r];
                 atomicOr(&bb[loc >> 5], 1u << (loc & 31));
               }
@@ -259,9 +260,9 @@ __global__ __launch_bounds__(kDBlock, kDecBlocksPerCU) void k_decode(DecodeArgs 
 #pragma unroll
             for (int r = 0; r < kDecR; ++r) {
               const uint32_t e = (uint32_t)(tid + r * kDBlock);
-              const uint32_t loc = cur.id[r] - (uint32_t)base;
+              const uint32_t loc = cur.id[r];
               const bool keep = pk.thresh == 0 ||
-                                comp_of(mag_key(cur.v[r]), cur.id[r], pk.ib) >= pk.thresh;
+                                comp_of(mag_key(cur.v[r]), (uint32_t)base + loc, pk.ib) >= pk.thresh;
               if (e < cntv && loc < (uint32_t)kChunk && keep) {
                 tile[loc] = cur.v[r];
                 atomicOr(&bb[loc >> 5], 1u << (loc & 31));
@@ -270,11 +271,11 @@ __global__ __launch_bounds__(kDBlock, kDecBlocksPerCU) void k_decode(DecodeArgs 
           }
           if (cntv > (uint32_t)(kDecR * kDBlock)) {              // dense slot (uniform, rare)
             gf32* pval = (gf32*)pm.val + base;
-            gu32* pidx = (gu32*)pm.idx + base;
+            gu16* pidx = (gu16*)pm.idx + base;
             for (uint32_t e = (uint32_t)(kDecR * kDBlock + tid); e < cntv; e += kDBlock) {
-              const uint32_t id = pidx[e];
+              const uint32_t loc = pidx[e];
+              const uint32_t id = (uint32_t)base + loc;
               const float v = pval[e];
-              const uint32_t loc = id - (uint32_t)base;
               if (loc < (uint32_t)kChunk && entry_kept(pk, id, v)) {
                 tile[loc] = scale ? (float)((double)v / pk.p) : v;
                 atomicOr(&bb[loc >> 5], 1u << (loc & 31));
@@ -390,15 +391,12 @@ constexpr int kSR = 4;                         // entries per thread per item (1
 #ifndef FC_SGROUP
 #define FC_SGROUP 4
 #endif
-#ifndef FC_DEC_PIPE
-#define FC_DEC_PIPE 1
-#endif
 constexpr int kSGroup = FC_SGROUP;             // items whose loads are issued together
 constexpr int kSBlocksPerCU = 3;               // 47 KB LDS per workgroup (4 per CU with the
                                                // poison counts dropped measured no faster)
 
 struct SparseMeta {
-  const uint32_t* idx;
+  const void* idx;            // uint16 chunk-local indices
   const float* val;
   const uint32_t* cnt;
   uint64_t seed, offset;
@@ -410,7 +408,7 @@ struct SparseMeta {
 
 __device__ __forceinline__ PktCache meta_pkt_s(const SparseMeta& pm) {
   PktCache c;
-  c.idx = pm.idx; c.val = pm.val; c.bitmap = pm.idx; c.cnt = pm.cnt; c.w = pm.w;
+  c.idx = pm.idx; c.val = pm.val; c.bitmap = nullptr; c.cnt = pm.cnt; c.w = pm.w;
   c.thresh = pm.thresh;
   c.ib = pm.flags & 0xffu; c.codec = (pm.flags >> 8) & 0xffu; c.key_mode = (pm.flags >> 16) & 0xffu;
   c.seed = pm.seed; c.offset = pm.offset; c.p = pm.p;
@@ -495,7 +493,6 @@ __global__ __launch_bounds__(kSBlock, kSBlocksPerCU) void k_decode_sparse(Decode
   auto load_cnt = [&](uint32_t m, uint32_t c) -> uint32_t {     // uniform value, vector load
     return ((gu32*)uni_ptr(s_meta[m].cnt))[c];
   };
-#if FC_DEC_PIPE
   // Two-slot software pipeline (loads issued in the order C0 C1 E0 | C2 E1 P0 | C3 E2 P1 ...,
   // C = slot counts of a group of items, E = its entries, P = its fold): the entries of group
   // g+1 are in flight while group g is folded, and every wait is a partial vmcnt (E_g is older
@@ -518,7 +515,7 @@ __global__ __launch_bounds__(kSBlock, kSBlocksPerCU) void k_decode_sparse(Decode
       const SparseMeta& pm = s_meta[im_[sl][d]];
       const uint64_t lo = (uint64_t)ic_[sl][d] * kChunk;
       gf32* val = (gf32*)uni_ptr(pm.val) + lo;
-      gu32* idx = (gu32*)uni_ptr(pm.idx) + lo;
+      gu16* idx = (gu16*)uni_ptr(pm.idx) + lo;
       cn_[sl][d] = uni32(cntg[sl][d]);
       const uint32_t last = cn_[sl][d] ? cn_[sl][d] - 1 : 0u;
 #pragma unroll
@@ -550,8 +547,7 @@ __global__ __launch_bounds__(kSBlock, kSBlocksPerCU) void k_decode_sparse(Decode
       const uint32_t key_mode = (flags >> 16) & 0xffu, poison = flags >> 24;
       const bool scale = codec == FC_CODEC_DROPOUT_UNBIASED;     // fl32(fl64(g)/p), :60
       const bool generic = scale || (key_mode == FC_KEY_PHILOX && thresh != 0);
-      auto fold = [&](uint32_t id, float v) {
-        const uint32_t loc = id - (uint32_t)base;
+      auto fold = [&](uint32_t loc, float v) {                   // chunk-local index
         if (loc >= (uint32_t)kChunk) return;
         if (ACC) {
           const float term = __fmul_rn(v, w);
@@ -571,9 +567,8 @@ __global__ __launch_bounds__(kSBlock, kSBlocksPerCU) void k_decode_sparse(Decode
 #pragma unroll
         for (int r = 0; r < kSR; ++r) {
           const uint32_t e = (uint32_t)(tid + r * kSBlock);
-          const uint32_t id = ids[d][r];
-          const bool keep = thresh == 0 || comp_of(mag_key(vs[d][r]), id, ib) >= thresh;
-          loc[r] = id - (uint32_t)base;
+          loc[r] = ids[d][r];
+          const bool keep = thresh == 0 || comp_of(mag_key(vs[d][r]), (uint32_t)base + loc[r], ib) >= thresh;
           ok[r] = e < cn[d] && keep && loc[r] < (uint32_t)kChunk;
           tv[r] = 0.f;
           if (ACC && ok[r]) tv[r] = tile[loc[r]];
@@ -593,19 +588,19 @@ __global__ __launch_bounds__(kSBlock, kSBlocksPerCU) void k_decode_sparse(Decode
         const PktCache pk = meta_pkt_s(pm);
         for (int r = 0; r < kSR; ++r) {
           const uint32_t e = (uint32_t)(tid + r * kSBlock);
-          const uint32_t id = ids[d][r];
+          const uint32_t lc = ids[d][r];
           const float v = vs[d][r];
-          if (e < cn[d] && entry_kept(pk, id, v)) fold(id, scale ? (float)((double)v / pk.p) : v);
+          if (e < cn[d] && entry_kept(pk, (uint32_t)base + lc, v)) fold(lc, scale ? (float)((double)v / pk.p) : v);
         }
       }
       if (cn[d] > (uint32_t)(kSR * kSBlock)) {                   // dense slot (uniform, rare)
         const PktCache pk = meta_pkt_s(pm);
         gf32* pval = (gf32*)uni_ptr(pm.val) + base;
-        gu32* pidx = (gu32*)uni_ptr(pm.idx) + base;
+        gu16* pidx = (gu16*)uni_ptr(pm.idx) + base;
         for (uint32_t e = (uint32_t)(kSR * kSBlock + tid); e < cn[d]; e += kSBlock) {
-          const uint32_t id = pidx[e];
+          const uint32_t lc = pidx[e];
           const float v = pval[e];
-          if (entry_kept(pk, id, v)) fold(id, scale ? (float)((double)v / pk.p) : v);
+          if (entry_kept(pk, (uint32_t)base + lc, v)) fold(lc, scale ? (float)((double)v / pk.p) : v);
         }
         __builtin_amdgcn_s_waitcnt(0x0F70);                      // vmcnt(0): none left pending
       }
@@ -636,129 +631,6 @@ __global__ __launch_bounds__(kSBlock, kSBlocksPerCU) void k_decode_sparse(Decode
     process(1, t0 + kSGroup);
   }
 }
-#else
-  uint32_t gm[kSGroup], gc[kSGroup], cntg[kSGroup];
-#pragma unroll
-  for (int d = 0; d < kSGroup; ++d) {
-    next_item(gm[d], gc[d]);
-    cntg[d] = load_cnt(gm[d], gc[d]);
-  }
-
-  init_tile(blockIdx.x);
-  __syncthreads();
-  for (uint32_t t0 = 0; t0 < T; t0 += kSGroup) {
-    uint32_t ids[kSGroup][kSR];
-    float vs[kSGroup][kSR];
-    uint32_t cn[kSGroup], im[kSGroup], ic[kSGroup];
-#pragma unroll
-    for (int d = 0; d < kSGroup; ++d) {
-      im[d] = gm[d]; ic[d] = gc[d];
-      const SparseMeta& pm = s_meta[im[d]];
-      const uint64_t lo = (uint64_t)ic[d] * kChunk;
-      gf32* val = (gf32*)uni_ptr(pm.val) + lo;
-      gu32* idx = (gu32*)uni_ptr(pm.idx) + lo;
-      cn[d] = uni32(cntg[d]);
-      const uint32_t last = cn[d] ? cn[d] - 1 : 0u;
-#pragma unroll
-      for (int r = 0; r < kSR; ++r) {
-        const uint32_t e = min((uint32_t)(tid + r * kSBlock), last);
-        vs[d][r] = val[e];
-        ids[d][r] = idx[e];
-      }
-    }
-#pragma unroll
-    for (int d = 0; d < kSGroup; ++d) {                          // next group's counts
-      next_item(gm[d], gc[d]);
-      cntg[d] = load_cnt(gm[d], gc[d]);
-    }
-#pragma unroll
-    for (int d = 0; d < kSGroup; ++d) {
-      const uint32_t t = t0 + d;
-      if (t >= T) break;                                         // uniform
-      const uint32_t m = im[d];
-      const uint32_t c = ic[d];
-      const uint64_t base = (uint64_t)c * kChunk;
-      const SparseMeta pm = s_meta[m];
-      const float w = __uint_as_float(uni32(__float_as_uint(pm.w)));
-      const uint64_t thresh = uni64(pm.thresh);
-      const uint32_t flags = uni32(pm.flags);
-      const uint32_t ib = flags & 0xffu, codec = (flags >> 8) & 0xffu;
-      const uint32_t key_mode = (flags >> 16) & 0xffu, poison = flags >> 24;
-      const bool scale = codec == FC_CODEC_DROPOUT_UNBIASED;     // fl32(fl64(g)/p), :60
-      const bool generic = scale || (key_mode == FC_KEY_PHILOX && thresh != 0);
-      auto fold = [&](uint32_t id, float v) {
-        const uint32_t loc = id - (uint32_t)base;
-        if (loc >= (uint32_t)kChunk) return;
-        if (ACC) {
-          const float term = __fmul_rn(v, w);
-          const float s2 = __fadd_rn(tile[loc], term);
-          tile[loc] = s2;
-          if (poison) cntC[loc] = (uint8_t)(cntC[loc] + 1u);
-        } else {
-          tile[loc] = v;
-        }
-      };
-      if (!generic) {                                            // top-k / dropout-biased
-        // a packet's locations are distinct: all tile reads first, then all writes (one LDS
-        // round trip per item, not one per entry)
-        uint32_t loc[kSR];
-        bool ok[kSR];
-        float tv[kSR];
-#pragma unroll
-        for (int r = 0; r < kSR; ++r) {
-          const uint32_t e = (uint32_t)(tid + r * kSBlock);
-          const uint32_t id = ids[d][r];
-          const bool keep = thresh == 0 || comp_of(mag_key(vs[d][r]), id, ib) >= thresh;
-          loc[r] = id - (uint32_t)base;
-          ok[r] = e < cn[d] && keep && loc[r] < (uint32_t)kChunk;
-          tv[r] = 0.f;
-          if (ACC && ok[r]) tv[r] = tile[loc[r]];
-        }
-#pragma unroll
-        for (int r = 0; r < kSR; ++r) {
-          if (!ok[r]) continue;
-          if (ACC) {
-            const float s2 = __fadd_rn(tv[r], __fmul_rn(vs[d][r], w));
-            tile[loc[r]] = s2;
-            if (poison) cntC[loc[r]] = (uint8_t)(cntC[loc[r]] + 1u);
-          } else {
-            tile[loc[r]] = vs[d][r];
-          }
-        }
-      } else {
-        const PktCache pk = meta_pkt_s(pm);
-        for (int r = 0; r < kSR; ++r) {
-          const uint32_t e = (uint32_t)(tid + r * kSBlock);
-          const uint32_t id = ids[d][r];
-          const float v = vs[d][r];
-          if (e < cn[d] && entry_kept(pk, id, v)) fold(id, scale ? (float)((double)v / pk.p) : v);
-        }
-      }
-      if (cn[d] > (uint32_t)(kSR * kSBlock)) {                   // dense slot (uniform, rare)
-        const PktCache pk = meta_pkt_s(pm);
-        gf32* pval = (gf32*)uni_ptr(pm.val) + base;
-        gu32* pidx = (gu32*)uni_ptr(pm.idx) + base;
-        for (uint32_t e = (uint32_t)(kSR * kSBlock + tid); e < cn[d]; e += kSBlock) {
-          const uint32_t id = pidx[e];
-          const float v = pval[e];
-          if (entry_kept(pk, id, v)) fold(id, scale ? (float)((double)v / pk.p) : v);
-        }
-        __builtin_amdgcn_s_waitcnt(0x0F70);                      // vmcnt(0): none left pending
-      }
-      __syncthreads();                                           // packet m folded
-      if (m + 1 == M) {                                          // chunk done
-        write_tile(c);
-        const uint32_t cnext = c + G;
-        if (t + 1 < T) {
-          __syncthreads();                                       // write-out read the tile
-          init_tile(cnext);
-          __syncthreads();
-        }
-      }
-    }
-  }
-}
-#endif
 
 // --------------------------------------------------------------------------------------
 // k_fold_q: the FedAVG fold of FC_FMT_IDXVAL packets (aggregation.py:61-63 + gar.py:44) with
@@ -786,7 +658,7 @@ constexpr int kQR = FC_QR;                      // entry rounds (x64 lanes) load
 constexpr int kQGroup = FC_QG;                  // items per load group
 
 struct QMeta {
-  const uint32_t* idx;
+  const void* idx;                              // uint16 chunk-local indices
   const float* val;
   const uint64_t* qoff;
   const fc_packet_hdr* hdr;
@@ -881,11 +753,11 @@ __global__ __launch_bounds__(kQBlock, 4) void k_fold_q(DecodeArgs a) {
       pk.codec = (uni32(pm.flags) >> 8) & 0xffu; pk.key_mode = (uni32(pm.flags) >> 16) & 0xffu;
       pk.seed = h->seed; pk.offset = h->offset; pk.p = h->p;
       const float w = __uint_as_float(uni32(__float_as_uint(pm.w)));
-      gu32* pidx = (gu32*)uni_ptr(pm.idx) + base;
+      gu16* pidx = (gu16*)uni_ptr(pm.idx) + base;
       gf32* pval = (gf32*)uni_ptr(pm.val) + base;
       if (uni32(pm.flags) >> 24) {              // poisoning: NaN where this packet folds nothing
         for (uint32_t e = st + lane; e < en; e += 64) {
-          const uint32_t id = pidx[e];
+          const uint32_t id = (uint32_t)base + pidx[e];
           const uint32_t loc = id - qbase;
           if (loc < (uint32_t)kQuarter && entry_kept(pk, id, pval[e]))
             atomicOr(&s_mark[q][loc >> 5], 1u << (loc & 31));
@@ -895,7 +767,8 @@ __global__ __launch_bounds__(kQBlock, 4) void k_fold_q(DecodeArgs a) {
           if (!((bits >> b) & 1u)) qt[lane * 32 + b] = __uint_as_float(0x7fc00000u);
         s_mark[q][lane] = 0u;
       }
-      for (uint32_t e = st + lane; e < en; e += 64) fold_q_entry(pk, w, qt, qbase, pidx[e], pval[e]);
+      for (uint32_t e = st + lane; e < en; e += 64)
+        fold_q_entry(pk, w, qt, qbase, (uint32_t)base + pidx[e], pval[e]);
     }
   } else {
     // ---- fast body: top-k / mask-selected packets; two register slots of kQGroup items, the
@@ -912,7 +785,7 @@ __global__ __launch_bounds__(kQBlock, 4) void k_fold_q(DecodeArgs a) {
         st_[sl][d] = st; en_[sl][d] = en;
         const QMeta& pm = s_meta[m];
         gf32* val = (gf32*)uni_ptr(pm.val) + base;
-        gu32* idx = (gu32*)uni_ptr(pm.idx) + base;
+        gu16* idx = (gu16*)uni_ptr(pm.idx) + base;
         const uint32_t last = en > st ? en - 1 : st;
 #pragma unroll
         for (int r = 0; r < kQR; ++r) {
@@ -937,11 +810,11 @@ __global__ __launch_bounds__(kQBlock, 4) void k_fold_q(DecodeArgs a) {
         float tv[kQR];
 #pragma unroll
         for (int r = 0; r < kQR; ++r) {                           // all tile reads, then writes
-          const uint32_t id = ids_[sl][d][r];
+          const uint32_t lc = ids_[sl][d][r];                     // chunk-local
           const float v = vs_[sl][d][r];
-          loc[r] = id - qbase;
+          loc[r] = lc - (uint32_t)(q * kQuarter);
           ok[r] = st + (uint32_t)(lane + r * 64) < en && loc[r] < (uint32_t)kQuarter &&
-                  (thresh == 0 || comp_of(mag_key(v), id, ib) >= thresh);
+                  (thresh == 0 || comp_of(mag_key(v), (uint32_t)base + lc, ib) >= thresh);
           tv[r] = ok[r] ? qt[loc[r]] : 0.f;
         }
 #pragma unroll
@@ -1036,8 +909,6 @@ template __global__ void k_decode<FC_FMT_IDXVAL, false, false>(DecodeArgs);
 template __global__ void k_decode<FC_FMT_IDXVAL, false, true>(DecodeArgs);
 template __global__ void k_decode<FC_FMT_BITMAP, false, false>(DecodeArgs);
 template __global__ void k_decode<FC_FMT_BITMAP, false, true>(DecodeArgs);
-template __global__ void k_decode<FC_FMT_IDXVAL, true, false>(DecodeArgs);
-template __global__ void k_decode_sparse<true>(DecodeArgs);
 template __global__ void k_fold_q<false>(DecodeArgs);
 template __global__ void k_fold_q<true>(DecodeArgs);
 template __global__ void k_decode_sparse<false>(DecodeArgs);

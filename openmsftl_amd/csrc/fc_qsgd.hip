@@ -191,7 +191,7 @@ __global__ __launch_bounds__(kBlock) void k_qsgd_decode(QsgdDecodeArgs a) {
       const fc_packet_hdr* h = v.hdr;
       const QsgdParams q = qsgd_params(h->p, (int)h->k, n);
       uint32_t c[8];
-      qsgd_unpack(v.idx, t, q.width, c);
+      qsgd_unpack(static_cast<const uint32_t*>(v.idx), t, q.width, c);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float d = qsgd_value(c[j], q);

@@ -400,7 +400,7 @@ struct CompactArgs {
   uint64_t bern_thr;        // kPredBern: keep iff word < thr
   uint32_t nonfinite_keep;  // dropout: dropped inf/NaN are listed as NaN (g * 0 == NaN)
   uint32_t write_hdr;       // mask pipelines (no earlier kernel) write the static header
-  uint32_t* idx;
+  uint16_t* idx;            // chunk-local indices (ABI 3)
   float* val;
   uint32_t* bitmap;
   uint32_t* cnt;            // entries per chunk
@@ -613,7 +613,7 @@ __global__ __launch_bounds__(kCBlock, FC_COMPACT_WAVES_PER_EU) void k_compact(Co
         if ((pbits >> (i * 4 + j)) & 1u) {
           float v = f4get(x[i], j);
           if (PRED != kPredKey && ((cbits >> (i * 4 + j)) & 1u)) v = __uint_as_float(0x7fc00000u);
-          if (FMT == FC_FMT_IDXVAL) a.idx[slot + pos] = e0 + j;
+          if (FMT == FC_FMT_IDXVAL) a.idx[slot + pos] = (uint16_t)(e0 + j - base);
           a.val[slot + pos] = v;
           ++pos;
         }
@@ -651,13 +651,13 @@ __global__ __launch_bounds__(kCBlock, FC_COMPACT_WAVES_PER_EU) void k_compact(Co
       if (t + 4 <= tot_e) {
         const uint4 p0 = *reinterpret_cast<const uint4*>(&st[t]);
         const uint4 p1 = *reinterpret_cast<const uint4*>(&st[t + 2]);
-        if (FMT == FC_FMT_IDXVAL)
-          *reinterpret_cast<uint4*>(a.idx + slot + t) =
-              make_uint4(base + p0.x, base + p0.z, base + p1.x, base + p1.z);
+        if (FMT == FC_FMT_IDXVAL)      // 4 chunk-local u16 indices: one 8-B store
+          *reinterpret_cast<uint2*>(a.idx + slot + t) =
+              make_uint2(p0.x | (p0.z << 16), p1.x | (p1.z << 16));
         *reinterpret_cast<uint4*>(a.val + slot + t) = make_uint4(p0.y, p0.w, p1.y, p1.w);
       } else {
         for (uint32_t u = t; u < tot_e; ++u) {
-          if (FMT == FC_FMT_IDXVAL) a.idx[slot + u] = base + st[u].x;
+          if (FMT == FC_FMT_IDXVAL) a.idx[slot + u] = (uint16_t)st[u].x;
           a.val[slot + u] = __uint_as_float(st[u].y);
         }
       }
@@ -758,7 +758,7 @@ __device__ __forceinline__ void mag_exact_bits(const MagPred& P, float (&x)[MagG
 // full CompactArgs of two items live across the loop spilled ~130 SGPRs.
 struct MagOut {
   const float* g;
-  uint32_t* idx;
+  uint16_t* idx;
   float* val;
   uint32_t* cnt;
   uint64_t* qoff;
@@ -847,7 +847,7 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
       const bool p = mag_listed<FAST>(P, x[q]);
       const uint32_t pos = prefix_count(__ballot(p)) + goff_of(q);
       if (p) {
-        a.idx[slot + pos] = base + FC_LOC(q);
+        a.idx[slot + pos] = (uint16_t)FC_LOC(q);
         a.val[slot + pos] = FAST ? x[q] : a.g[base + FC_LOC(q)];
       }
       dense_out(q, p);
@@ -891,12 +891,12 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
       if (t + 4 <= tot_e) {
         const uint4 p0 = *reinterpret_cast<const uint4*>(&sh.st[t]);
         const uint4 p1 = *reinterpret_cast<const uint4*>(&sh.st[t + 2]);
-        *reinterpret_cast<uint4*>(a.idx + slot + t) =
-            make_uint4(base + p0.x, base + p0.z, base + p1.x, base + p1.z);
+        *reinterpret_cast<uint2*>(a.idx + slot + t) =      // 4 chunk-local u16 indices
+            make_uint2(p0.x | (p0.z << 16), p1.x | (p1.z << 16));
         *reinterpret_cast<uint4*>(a.val + slot + t) = make_uint4(p0.y, p0.w, p1.y, p1.w);
       } else {
         for (uint32_t u = t; u < tot_e; ++u) {
-          a.idx[slot + u] = base + sh.st[u].x;
+          a.idx[slot + u] = (uint16_t)sh.st[u].x;
           a.val[slot + u] = __uint_as_float(sh.st[u].y);
         }
       }
@@ -948,7 +948,7 @@ __device__ __forceinline__ MagOut mag_out(const CompactArgs& a0, uint32_t client
   o.dense = a0.jobs ? nullptr : a0.dense;
   if (a0.jobs) {                                // {g, idx, val, cnt} = first 32 B of the job
     const fc_u32x8 v = sload8(&a0.jobs[client]);
-    o.g = as_ptr<const float>(v[0], v[1]); o.idx = as_ptr<uint32_t>(v[2], v[3]);
+    o.g = as_ptr<const float>(v[0], v[1]); o.idx = as_ptr<uint16_t>(v[2], v[3]);
     o.val = as_ptr<float>(v[4], v[5]); o.cnt = as_ptr<uint32_t>(v[6], v[7]);
     const fc_u32x2 qv = sload2(&a0.jobs[client].qoff);
     o.qoff = as_ptr<uint64_t>(qv.x, qv.y);
@@ -1166,7 +1166,7 @@ template __global__ void k_fused_mag<true>(CompactArgs, SamplePlan, HdrInit, uin
 struct ResolveArgs {
   uint32_t ib, nchunks;
   uint64_t k;
-  const uint32_t* idx;      // packet (for overflowed candidate slots)
+  const uint16_t* idx;      // packet (for overflowed candidate slots), chunk-local
   const float* val;
   const uint32_t* cnt;
   uint64_t seed, offset;
@@ -1272,7 +1272,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve(ResolveArgs a0) {
               v[u] = a.W.cand[(uint64_t)c * kCandSlot + r];
             } else {
               const uint64_t p = (uint64_t)c * kChunk + r;
-              const uint32_t id = a.idx[p];
+              const uint32_t id = c * (uint32_t)kChunk + a.idx[p];
               const uint32_t key = a.key_mode == FC_KEY_PHILOX ? (philox_word(id, a.seed, a.offset) >> 1)
                                                                : mag_key(a.val[p]);
               v[u] = (key >= t_lo && key <= t_hi) ? comp_of(key, id, a.ib) : ~0ull;

@@ -28,7 +28,7 @@ def _gpu():
         pytest.skip("no GPU")
     from openmsftl_amd import _lib
     lib = _lib.load()
-    assert lib.fc_abi_version() == 2
+    assert lib.fc_abi_version() == 3
 
 
 def _codec():
@@ -249,7 +249,8 @@ def test_top_128M_properties():
     assert float(a[nz].min()) >= float(a[~nz].max())         # every kept >= every dropped
     pos = torch.arange(pkt.capacity, device="cuda")
     listed = (pos % 8192) < pkt.cnt.to(torch.int64)[pos // 8192]
-    idx = pkt.idx[listed].to(torch.int64)
+    # chunk-local uint16 indices (int16 storage) + the slot's chunk base = element index
+    idx = (pkt.idx[listed].to(torch.int64) & 0xffff) + (pos[listed] // 8192) * 8192
     assert idx.numel() == h.n_entries
     assert bool((idx[1:] > idx[:-1]).all())                  # ascending packet (slot order)
     # slack stays small (the packet carries few unselected entries)
