@@ -32,6 +32,12 @@ __global__ __launch_bounds__(256) void k_write16(uint4* out) {
   out[i] = make_uint4((uint32_t)i, 1u, 2u, 3u);
 }
 
+// k_compact_mag1's packet index stores since ABI 3: 8 B per lane (4 uint16 indices), coalesced.
+__global__ __launch_bounds__(256) void k_write8(uint2* out) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  out[i] = make_uint2((uint32_t)i, 1u);
+}
+
 // k_compact_mag1_dense's q stores: 4 B per lane in the read layout, non-temporal.
 __global__ __launch_bounds__(512) void k_write4_nt(float* out) {
   const uint32_t base = blockIdx.x * 8192u + (threadIdx.x >> 6) * 256u + (threadIdx.x & 63u);
@@ -45,6 +51,7 @@ extern "C" int pmc_calib_run(int which, void* buf, uint64_t nfloats, void* sink)
     case 1: hipLaunchKernelGGL(k_read16, dim3((uint32_t)(nfloats / 1024)), dim3(256), 0, 0, (const float4*)buf, (float*)sink); break;
     case 2: hipLaunchKernelGGL(k_write16, dim3((uint32_t)(nfloats / 1024)), dim3(256), 0, 0, (uint4*)buf); break;
     case 3: hipLaunchKernelGGL(k_write4_nt, dim3((uint32_t)(nfloats / 8192)), dim3(512), 0, 0, (float*)buf); break;
+    case 4: hipLaunchKernelGGL(k_write8, dim3((uint32_t)(nfloats / 512)), dim3(256), 0, 0, (uint2*)buf); break;
     default: return -1;
   }
   return hipGetLastError() == hipSuccess ? 0 : -2;

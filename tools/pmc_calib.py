@@ -19,7 +19,7 @@ def main():
     lib.pmc_calib_run.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
     buf = torch.randn(NFLOATS, device="cuda")
     sink = torch.zeros(1 << 20, device="cuda")
-    for which in range(4):
+    for which in range(5):
         for _ in range(3):
             assert lib.pmc_calib_run(which, ctypes.c_void_p(buf.data_ptr()), NFLOATS,
                                      ctypes.c_void_p(sink.data_ptr())) == 0

@@ -11,7 +11,7 @@ one kernel and converts them to HBM bytes per launch.  MI355X_MICROARCH.md §HBM
 FETCH_SIZE reports half the bytes of a wide (16 B/lane) streaming read and WRITE_SIZE is exact
 for 16 B/lane streaming stores; other widths must be calibrated on a known byte count.
 `calib` does that with tools/pmc_calib.hip's kernels (512 MiB each, k_compact_mag1's 4 B/lane
-non-temporal read and its store shapes) and `pmc --calib` applies the measured factors
+non-temporal read and its store shapes: 16 B/lane values, 8 B/lane uint16 indices) and `pmc --calib` applies the measured factors
 (read: k_read4_nt, write: k_write16) instead of the 16 B/lane defaults.
 """
 from __future__ import annotations
@@ -66,7 +66,8 @@ def calib(fetch_db, write_db, out):
     """Bytes / reported bytes for each calibration kernel (its known 512 MiB)."""
     res = {"known_bytes_per_dispatch": CALIB_BYTES, "source": "tools/pmc_calib.hip"}
     for kern, db, ctr in (("k_read4_nt", fetch_db, "FETCH_SIZE"), ("k_read16", fetch_db, "FETCH_SIZE"),
-                          ("k_write16", write_db, "WRITE_SIZE"), ("k_write4_nt", write_db, "WRITE_SIZE")):
+                          ("k_write16", write_db, "WRITE_SIZE"), ("k_write4_nt", write_db, "WRITE_SIZE"),
+                          ("k_write8", write_db, "WRITE_SIZE")):
         v = pmc_values(db, ctr, kern)
         if not v:
             raise SystemExit(f"no {ctr} for {kern}")
