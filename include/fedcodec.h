@@ -165,6 +165,18 @@ size_t fc_workspace_bytes_batch(uint64_t n, int m);
 int fc_topk_encode_batch(const fc_encode_job* jobs_dev, int m, uint64_t n, uint64_t k,
                          int key_mode, uint64_t capacity, void* ws, size_t ws_bytes,
                          fc_stream_t stream);
+/* The same pipeline in two parts on the caller's stream (the same jobs and ws for both):
+ * FC_PART_SAMPLE launches the bracket sample, which reads g and writes only the headers and
+ * the workspace; FC_PART_FINISH launches the compaction and the exact resolve, which write the
+ * packet buffers.  A caller that double-buffers the headers can therefore run the next
+ * batch's sample while the previous packets are still being read (fc_decode_accumulate), and
+ * order FC_PART_FINISH behind that fold.  part = FC_PART_SAMPLE | FC_PART_FINISH is
+ * fc_topk_encode_batch. */
+#define FC_PART_SAMPLE 1
+#define FC_PART_FINISH 2
+int fc_topk_encode_batch_part(const fc_encode_job* jobs_dev, int m, uint64_t n, uint64_t k,
+                              int key_mode, uint64_t capacity, void* ws, size_t ws_bytes,
+                              int part, fc_stream_t stream);
 
 /* Exact radix-select path (several reads of g); always succeeds; n_entries == k. */
 int fc_topk_encode_exact(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_t seed,

@@ -19,6 +19,7 @@ FC_CODEC_TOP, FC_CODEC_RAND, FC_CODEC_DROPOUT_BIASED, FC_CODEC_DROPOUT_UNBIASED 
 FC_CODEC_QSGD = 5
 FC_KEY_MAGNITUDE, FC_KEY_PHILOX = 0, 1
 FC_FMT_IDXVAL, FC_FMT_BITMAP, FC_FMT_QSGD = 0, 1, 2
+FC_PART_SAMPLE, FC_PART_FINISH = 1, 2
 FC_CHUNK = 8192
 HDR_BYTES = 96
 
@@ -78,6 +79,7 @@ SIGNATURES = {
                                     _vp, _vp]),
     "fc_workspace_bytes_batch": (_sz, [_u64, _i32]),
     "fc_topk_encode_batch": (_i32, [_vp, _i32, _u64, _u64, _i32, _u64, _vp, _sz, _vp]),
+    "fc_topk_encode_batch_part": (_i32, [_vp, _i32, _u64, _u64, _i32, _u64, _vp, _sz, _i32, _vp]),
     "fc_topk_encode_exact": (_i32, [_vp, _u64, _u64, _i32, _u64, _u64, _vp, _vp, _u64, _vp,
                                     _vp, _vp, _vp, _sz, _vp]),
     "fc_mask_encode": (_i32, [_vp, _u64, _i32, _vp, _dbl, _u64, _u64, _i32, _vp, _vp, _vp,

@@ -264,12 +264,19 @@ def encode_top_batch(grads: Sequence[torch.Tensor], k: int, *,
                      key_mode: int = L.FC_KEY_MAGNITUDE, seeds=None, offsets=None,
                      packets: Optional[Sequence[Packet]] = None,
                      jobs: Optional[torch.Tensor] = None, check: bool = True,
-                     streams: int = 2, groups: Optional[Sequence[int]] = None) -> list:
+                     streams: int = 2, groups: Optional[Sequence[int]] = None,
+                     part: int = L.FC_PART_SAMPLE | L.FC_PART_FINISH, fork: bool = True,
+                     join: bool = True) -> list:
     """Top-k (or native rand-k) of M equal-length gradients in ONE launch per pipeline stage
     (fc_topk_encode_batch).  Same packets, bit for bit, as M calls of :func:`encode_top`.
     ``jobs``: a prebuilt :func:`encode_jobs` array for these exact grads/packets.
     ``streams``: sub-batches launched on that many forked streams (joined before return);
-    ``groups``: sub-batch sizes (default: ``streams`` equal parts), dealt to the streams in turn."""
+    ``groups``: sub-batch sizes (default: ``streams`` equal parts), dealt to the streams in turn.
+    Pipelining (bench.py): ``part`` = FC_PART_SAMPLE or FC_PART_FINISH runs one half of the
+    pipeline (fc_topk_encode_batch_part; the same ``groups`` / ``streams`` for both halves, so
+    each sub-batch's halves share a stream and its workspace); ``fork=False``: the forked
+    streams do not wait for the caller's stream first; ``join=False``: the caller's stream does
+    not wait for them (the caller orders later work itself)."""
     if not grads:
         raise ValueError("no gradients")
     lib = L.load()
@@ -287,6 +294,8 @@ def encode_top_batch(grads: Sequence[torch.Tensor], k: int, *,
         packets = [Packet.alloc(n, L.FC_FMT_IDXVAL, dev, k=k) for _ in range(m)]
     if len(packets) != m:
         raise ValueError("one packet per gradient")
+    if part != (L.FC_PART_SAMPLE | L.FC_PART_FINISH) and (k == 0 or k == n or n < 2 or check):
+        raise ValueError("a partial batch encode needs 0 < k < n and check=False")
     if k == 0 or k == n or n < 2:                    # trivial thresholds: exact engine per client
         return [encode_top(g, k, key_mode=key_mode, seed=s, offset=o, packet=p, check=check)
                 for g, p, s, o in zip(grads, packets, seeds, offsets)]
@@ -305,8 +314,8 @@ def encode_top_batch(grads: Sequence[torch.Tensor], k: int, *,
         raise ValueError(f"groups {groups} must be positive sizes summing to {m} clients")
     if nside == 1 or len(groups) == 1:
         ws = BatchWorkspace.get(n, m, dev)
-        L.check(lib.fc_topk_encode_batch(_vp(jobs), m, n, k, key_mode, packets[0].capacity,
-                                         _vp(ws.buf), ws.nbytes, _stream(dev)),
+        L.check(lib.fc_topk_encode_batch_part(_vp(jobs), m, n, k, key_mode, packets[0].capacity,
+                                              _vp(ws.buf), ws.nbytes, part, _stream(dev)),
                 "fc_topk_encode_batch")
     else:
         # Sub-batches on forked streams (group i on stream i % streams): one sub-batch's
@@ -315,24 +324,26 @@ def encode_top_batch(grads: Sequence[torch.Tensor], k: int, *,
         # tools/overlap_probe.py).  Packets are identical; the caller's stream joins every
         # fork before this returns, so later work (and frees) stay ordered.
         main = torch.cuda.current_stream(dev)
-        fork = torch.cuda.Event()
-        fork.record(main)
         job_bytes = ctypes.sizeof(L.EncodeJob)
         base = jobs.data_ptr()
         sides = _side_streams(dev, nside)
-        for side in sides:
-            side.wait_event(fork)
+        if fork:
+            ev = torch.cuda.Event()
+            ev.record(main)
+            for side in sides:
+                side.wait_event(ev)
         lo = 0
         for i, size in enumerate(groups):
             with torch.cuda.stream(sides[i % nside]):
                 ws = BatchWorkspace.get(n, size, dev)
-                L.check(lib.fc_topk_encode_batch(ctypes.c_void_p(base + lo * job_bytes), size,
-                                                 n, k, key_mode, packets[0].capacity,
-                                                 _vp(ws.buf), ws.nbytes, _stream(dev)),
+                L.check(lib.fc_topk_encode_batch_part(ctypes.c_void_p(base + lo * job_bytes),
+                                                      size, n, k, key_mode, packets[0].capacity,
+                                                      _vp(ws.buf), ws.nbytes, part, _stream(dev)),
                         "fc_topk_encode_batch")
             lo += size
-        for side in sides:
-            main.wait_stream(side)
+        if join:
+            for side in sides:
+                main.wait_stream(side)
     if check:
         resolve(packets)
     return list(packets)

@@ -386,6 +386,14 @@ size_t fc_workspace_bytes_batch(uint64_t n, int m) {
 int fc_topk_encode_batch(const fc_encode_job* jobs, int m, uint64_t n, uint64_t k,
                          int key_mode, uint64_t capacity, void* ws, size_t ws_bytes,
                          fc_stream_t stream) {
+  return fc_topk_encode_batch_part(jobs, m, n, k, key_mode, capacity, ws, ws_bytes,
+                                   FC_PART_SAMPLE | FC_PART_FINISH, stream);
+}
+
+int fc_topk_encode_batch_part(const fc_encode_job* jobs, int m, uint64_t n, uint64_t k,
+                              int key_mode, uint64_t capacity, void* ws, size_t ws_bytes,
+                              int part, fc_stream_t stream) {
+  FC_CHECK(part >= 1 && part <= (FC_PART_SAMPLE | FC_PART_FINISH), "bad part %d", part);
   FC_CHECK(jobs != nullptr, "jobs is NULL");
   FC_CHECK(m >= 1 && m <= 65535, "m=%d outside [1, 65535]", m);
   FC_CHECK(n >= 2 && n <= 0xffffffffull, "n=%llu outside [2, 2^32-1]", (unsigned long long)n);
@@ -416,8 +424,11 @@ int fc_topk_encode_batch(const fc_encode_job* jobs, int m, uint64_t n, uint64_t 
   hipStream_t s = (hipStream_t)stream;
   const SamplePlan P = make_plan(n, k);
   const dim3 sgrid((P.nseg + kSampleSegs - 1) / kSampleSegs, (uint32_t)m);
-  int rc = launch_sample(key_mode, sgrid, nullptr, P, 0ull, 0ull, ca.W, ib, nullptr, hi, jobs, stride, s);
-  if (rc) return rc;
+  if (part & FC_PART_SAMPLE) {
+    int rc = launch_sample(key_mode, sgrid, nullptr, P, 0ull, 0ull, ca.W, ib, nullptr, hi, jobs, stride, s);
+    if (rc) return rc;
+  }
+  if (!(part & FC_PART_FINISH)) return FC_OK;
   {
     TimedLaunch t(FC_TIME_COMPACT, s);
     const dim3 grid(ca.nchunks, (uint32_t)m);

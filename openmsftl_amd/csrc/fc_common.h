@@ -23,7 +23,10 @@ constexpr int kSmallCap = 4096;             // exact-finish list (LDS bitonic, 3
 constexpr int kEngineGrid = 256;            // radix-engine workgroups (one per CU)
 constexpr int kEnginePasses = 6;            // ceil(63 / 12): enough for any comp width
 constexpr int kResolveGrid = 256;           // k_resolve workgroups
-constexpr int kResolveGridBatch = 64;       // k_resolve workgroups per client (batched encode)
+#ifndef FC_RESOLVE_GRID_BATCH
+#define FC_RESOLVE_GRID_BATCH 64
+#endif
+constexpr int kResolveGridBatch = FC_RESOLVE_GRID_BATCH;   // k_resolve workgroups per client (batched encode)
 constexpr int kSlots = kVec * kWaves;       // 32 (i, w) slots per chunk
 constexpr int kCandSlot = 256;              // candidate slot per chunk (overflow: re-read entries)
 constexpr int kShards = 64;                 // sharded k_compact totals

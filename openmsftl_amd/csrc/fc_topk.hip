@@ -328,7 +328,9 @@ __device__ __forceinline__ void sample_body(const float* __restrict__ g, const S
     for (int j = 0; j < kPer; ++j) h[j * kBlock + tid] = t[j];
   }
   __syncthreads();
+  FC_TR(7);
   find_ranks_desc(h, P.hi_none ? 1u : (uint32_t)P.r_hi, P.lo_all ? 1u : (uint32_t)P.r_lo, s_tmp, s_out);
+  FC_TR(23);
   const uint32_t t_hi = P.hi_none ? 0xffffffffu : fine_upper(s_out[0], F);
   const uint32_t t_lo = P.lo_all ? 0u : fine_lower(s_out[2], F);
   // the state k_compact reads; sc1 stores from wave 0 so that a publication (pub) after its

@@ -279,6 +279,30 @@ def test_batch_encode_equals_single(n, f, M):
         _check_top_packet(x, k, pb, codec.decode(pb).cpu().numpy())
 
 
+@pytest.mark.parametrize("streams", [1, 2])
+def test_batch_encode_in_two_parts(streams):
+    """fc_topk_encode_batch_part: the sample part, then (after unrelated work on the caller's
+    stream) the finish part, gives the packets of one fc_topk_encode_batch call."""
+    from openmsftl_amd import _lib as L
+    codec = _codec()
+    n, M = 300_001, 5
+    rng = np.random.default_rng(77)
+    grads = [torch.from_numpy((rng.standard_normal(n) * 10.0 ** rng.uniform(-4, 1))
+                              .astype(np.float32)).cuda() for _ in range(M)]
+    k = co.num_kept(0.1, n)
+    want = [_packet_bytes(p) for p in codec.encode_top_batch(grads, k, streams=streams)]
+    pk = [codec.Packet.alloc(n, L.FC_FMT_IDXVAL, grads[0].device, k=k) for _ in range(M)]
+    codec.encode_top_batch(grads, k, packets=pk, check=False, streams=streams,
+                           part=L.FC_PART_SAMPLE, fork=False, join=False)
+    torch.ones(1 << 20, device="cuda").sum()                   # caller-stream work in between
+    codec.encode_top_batch(grads, k, packets=pk, check=False, streams=streams,
+                           part=L.FC_PART_FINISH)
+    torch.cuda.synchronize()
+    assert [_packet_bytes(p) for p in pk] == want
+    with pytest.raises(ValueError):
+        codec.encode_top_batch(grads, k, packets=pk, part=L.FC_PART_SAMPLE)   # check=True
+
+
 @pytest.mark.parametrize("M,n", [(65, 20_000), (70, 8_193 * 3), (130, 9_000)])
 def test_batch_encode_client_interleave(M, n):
     """k_compact_mag1 interleaves the chunks of 64 clients in dispatch order: a full group, a
