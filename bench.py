@@ -13,7 +13,7 @@ aggregate to rank 0.  Weak scaling: per-GPU work is fixed.
 
 Prints ONE JSON line on rank 0.  `value` = gradient bytes (4 N per client, all ranks) per
 second of step time; `roofline` = the encode pass k_compact_mag1 (the dominant kernel), algorithmic
-bytes 4N + 6k per client (ABI 3 packets: 6 B per entry) over its HIP-event-timed average launch duration, `traffic` from the
+bytes 4N + 8k per client (ABI-3 packets write 6 B per entry) over its HIP-event-timed average launch duration, `traffic` from the
 committed calibrated PMC summary; `cpu_baseline` = the reference's exact NumPy calls
 (compression.py:31-37, default argsort) on one 128 M gradient, with every BASELINE.md §3 row
 in `extra.cpu_baseline_matrix`.  A self-check outside the timed region re-encodes two clients
@@ -32,7 +32,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-ENTRY_BYTES = 6.0             # packet entry: uint16 chunk-local index + fp32 value (ABI 3)
+# SURVEY.md §8(d) prices a packet entry at 8 B (uint32 idx + fp32 val) in the algorithmic bytes
+# that roofline.achieved must use; ABI-3 packets actually carry 6 B (uint16 chunk-local index),
+# which the PMC `traffic` field shows (below the algorithmic bytes, not above)
+ENTRY_BYTES = 8.0
 
 
 def parse():
@@ -47,6 +50,7 @@ def parse():
                     help="forked streams the batched encode is split over (1 = one launch chain)")
     ap.add_argument("--roofline-steps", type=int, default=5,
                     help="extra encode passes with one stream, timed per launch for `roofline`")
+    ap.add_argument("--lib", default=None, help="A/B only: load this libfedcodec.so build")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-single", action="store_true", help="skip the single-gradient probe")
     ap.add_argument("--no-batch", action="store_true",
@@ -183,6 +187,8 @@ def main():
     torch.cuda.set_device(device)
 
     from openmsftl_amd import _lib as L
+    if args.lib:
+        L.load(os.path.abspath(args.lib))
     from openmsftl_amd import codec
     from openmsftl_amd.compression import kept_count
     from openmsftl_amd.distributed import ShardedFedAvg, fedavg_weights, packet_fold, shard_range
@@ -277,8 +283,7 @@ def main():
                                        streams=1)
             torch.cuda.synchronize()
     t_compact_us = kt_roof.avg_us("compact")
-    # the encode pass reads 4N and writes the k entries per client, 6 B each in
-    # the ABI-3 packet (uint16 chunk-local index + fp32 value; §8(d) priced 8 B with uint32)
+    # the encode pass reads 4N and writes the k entries, priced 8 B each
     alg_bytes = per_launch * (4.0 * n + ENTRY_BYTES * k)
     achieved = alg_bytes / (t_compact_us * 1e-6) / 1e9
     pmc, pmc_src = load_pmc(args.pmc)
@@ -300,8 +305,7 @@ def main():
                          if args.streams > 1 and not args.no_batch else "timed steps")
 
     # whole step against the HBM roofline (SURVEY §8(d) batched FedAvg with fused
-    # decode-accumulate: M (4N + 2 e k) + 4N algorithmic bytes per GPU and step, e = 6 B
-    # per packet entry)
+    # decode-accumulate: M (4N + 16k) + 4N algorithmic bytes per GPU and step)
     step_alg = M * (4.0 * n + 2 * ENTRY_BYTES * k) + 4.0 * n
     step_gbps = step_alg * world / (elapsed / args.steps) / 1e9
     extra = {"per_step_kernel_time": breakdown, "exact_fallbacks": redo_total[0],
@@ -350,7 +354,7 @@ def main():
 
 def single_gradient(torch, codec, g, k, n, iters=20):
     """North-star probe: encode+decode of ONE 128 M gradient (packet -> dense), HBM fraction
-    of the algorithmic 8N + 12k bytes (SURVEY §8(d) with 6-B packet entries)."""
+    of the algorithmic 8N + 16k bytes."""
     out = torch.empty_like(g)
     pkt = codec.encode_top(g, k)
     for _ in range(3):

@@ -107,7 +107,10 @@ struct SamplePlan {
   uint32_t pstride;    // their spacing = the sample grid (segment j*pstride, j < np)
   int64_t pr_hi, pr_lo;  // pilot ranks (1-based from the top) that bound the fine window
 };
-constexpr int kPilotSegs = 4;                 // = kSampleSegs: the pilot IS workgroup 0's share
+#ifndef FC_SAMPLE_SEGS_PER_WG
+#define FC_SAMPLE_SEGS_PER_WG 4
+#endif
+constexpr int kPilotSegs = FC_SAMPLE_SEGS_PER_WG;   // = kSampleSegs: the pilot IS workgroup 0's share
 constexpr uint64_t kFullSampleMax = 1ull << 20;
 
 __host__ __device__ __forceinline__ uint64_t seg_start(const SamplePlan& P, uint32_t s) {

@@ -133,9 +133,6 @@ __device__ void bitonic_desc(uint64_t* sv, uint32_t P2) {
 // candidates), it cannot make it wrong.  (Two launches — level 1 on key >> 19, level 2 on
 // (key >> 7) & 0xfff — took 17.8 + 21.5 us per 128 M gradient.)
 // --------------------------------------------------------------------------------------
-#ifndef FC_SAMPLE_SEGS_PER_WG
-#define FC_SAMPLE_SEGS_PER_WG 4
-#endif
 constexpr int kSampleSegs = FC_SAMPLE_SEGS_PER_WG;
 constexpr uint32_t kSpinMax = 1u << 18;   // bounded spins (~60 ms): one that never ends is a bug
 constexpr uint32_t kFineLo = 1024, kFineBins = 2048, kFineHi = kFineLo + kFineBins;

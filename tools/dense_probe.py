@@ -29,7 +29,7 @@ def main(n=134_217_728, f=0.1, iters=20):
     dt = (time.perf_counter() - t0) / iters
     redo = codec.resolve([pkt])
     print(json.dumps({"n": n, "k": k, "us": round(dt * 1e6, 1), "retry": redo,
-                      "alg_frac": round((8.0 * n + 12.0 * k) / dt / 8e12, 4)}), flush=True)
+                      "alg_frac": round((8.0 * n + 16.0 * k) / dt / 8e12, 4)}), flush=True)
 
 
 if __name__ == "__main__":

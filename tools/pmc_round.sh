@@ -20,5 +20,5 @@ timeout -s KILL 170 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_f -o pmc -- python3 t
 timeout -s KILL 170 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_w -o pmc -- python3 tools/kbench.py --batch 128 --iters 2 --tag pmc > $OUT/pmc_w.log 2>&1
 python3 tools/rocpd_summary.py pmc $(find $OUT/pmc_f -name "*.db" | head -1) \
   $(find $OUT/pmc_w -name "*.db" | head -1) k_compact_mag1 $OUT/pmc_k_compact_mag1.json \
-  --alg-bytes $((128 * (4 * N + 6 * K))) --clients-per-launch 128 --calib $OUT/pmc_calib.json
+  --alg-bytes $((128 * (4 * N + 8 * K))) --clients-per-launch 128 --calib $OUT/pmc_calib.json
 echo "[pmc] done"

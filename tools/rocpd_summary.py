@@ -4,6 +4,7 @@
     python tools/rocpd_summary.py pmc <fetch.db> <write.db> <kernel-substring> <out.json> \
         [--alg-bytes B] [--calib profiles/<tag>_pmc_calib.json]
     python tools/rocpd_summary.py calib <fetch.db> <write.db> <out.json>
+    python tools/rocpd_summary.py counters <db> <kernel-substring>
 
 `stats` is the per-kernel table rocprofv3 --stats prints (calls, total/avg/min/max ns, %).
 `pmc` averages FETCH_SIZE / WRITE_SIZE (kilobytes, one --pmc pass each) over the dispatches of
@@ -109,6 +110,16 @@ def pmc(fetch_db, write_db, substr, out, alg_bytes=None, clients=1, calib_path=N
     return res
 
 
+def counters(db, substr):
+    """Average of every collected counter over the dispatches of one kernel (name substring)."""
+    c = sqlite3.connect(db)
+    per = {}
+    for name, ctr, v in c.execute("select kernel_name, counter_name, value from counters_collection"):
+        if substr in name:
+            per.setdefault(ctr, []).append(float(v))
+    return {k: {"avg": statistics.mean(v), "dispatches": len(v)} for k, v in sorted(per.items())}
+
+
 def main():
     ap = argparse.ArgumentParser()
     sub = ap.add_subparsers(dest="cmd", required=True)
@@ -123,6 +134,9 @@ def main():
     p.add_argument("--alg-bytes", type=float, default=None)
     p.add_argument("--clients-per-launch", type=int, default=1)
     p.add_argument("--calib", default=None)
+    k = sub.add_parser("counters")
+    k.add_argument("db")
+    k.add_argument("kernel")
     c = sub.add_parser("calib")
     c.add_argument("fetch_db")
     c.add_argument("write_db")
@@ -131,6 +145,8 @@ def main():
     if a.cmd == "stats":
         for name, d in stats(a.db, a.out)[:12]:
             print(f"{len(d):7d} {sum(d) / len(d) / 1e3:10.2f} us  {name[:100]}")
+    elif a.cmd == "counters":
+        print(json.dumps(counters(a.db, a.kernel), indent=1))
     elif a.cmd == "calib":
         print(json.dumps(calib(a.fetch_db, a.write_db, a.out), indent=1))
     else:
