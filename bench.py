@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--roofline-steps", type=int, default=5,
                     help="extra encode passes with one stream, timed per launch for `roofline`")
     ap.add_argument("--lib", default=None, help="A/B only: load this libfedcodec.so build")
+    ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
+                    help="nccl (RCCL over xGMI: the measurement) or gloo (rehearsal only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-single", action="store_true", help="skip the single-gradient probe")
     ap.add_argument("--no-batch", action="store_true",
@@ -180,9 +182,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.backend == "gloo":
+        # rehearsal of the multi-rank path on fewer GPUs than ranks (ranks share devices; the
+        # partial sums are staged through host memory, distributed.py); never the measurement
+        local %= max(1, torch.cuda.device_count())
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
 
@@ -259,7 +268,8 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device=device if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_step = 1e3 * elapsed / args.steps
@@ -344,7 +354,8 @@ def main():
                                    "gradients, top-k f=0.1 encode -> FedAVG decode-accumulate"
                                    + (" -> RCCL reduce" if world > 1 else ""),
                        "clients_per_gpu": M, "n": n, "codec": "top", "fraction": f, "k": k,
-                       "parallelism": f"dp{world}"},
+                       "parallelism": f"dp{world}",
+                       **({"rehearsal": "gloo, ranks sharing GPUs"} if args.backend == "gloo" else {})},
             "roofline": roofline, "cpu_baseline": cpu, "extra": extra,
         }
         print(json.dumps(line), flush=True)
