@@ -74,6 +74,9 @@ static uint32_t decode_grid(uint64_t n, uint32_t per_cu = kDecBlocksPerCU) {
 #ifndef FC_MAX_SAMPLE_SEGS
 #define FC_MAX_SAMPLE_SEGS 1024
 #endif
+#ifndef FC_SAMPLE_DIV
+#define FC_SAMPLE_DIV 64                          // sample 1/64 of the gradient (below the cap)
+#endif
 static SamplePlan make_plan(uint64_t n, uint64_t k) {
   SamplePlan P;
   memset(&P, 0, sizeof P);
@@ -85,7 +88,7 @@ static SamplePlan make_plan(uint64_t n, uint64_t k) {
   } else {
     // 1/64 of the gradient, 64..1024 segments: at 16 M a 64-client batch spends 1391 us in
     // sample + compact + resolve with 256 segments against 1481 us with 512 (1/32)
-    uint64_t seg = n / 64 / 1024;
+    uint64_t seg = n / FC_SAMPLE_DIV / 1024;
     if (seg < 64) seg = 64;
     if (seg > FC_MAX_SAMPLE_SEGS) seg = FC_MAX_SAMPLE_SEGS;
     P.nseg = (uint32_t)seg;

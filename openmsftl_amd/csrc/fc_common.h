@@ -24,9 +24,10 @@ constexpr int kEngineGrid = 256;            // radix-engine workgroups (one per 
 constexpr int kEnginePasses = 6;            // ceil(63 / 12): enough for any comp width
 constexpr int kResolveGrid = 256;           // k_resolve workgroups
 #ifndef FC_RESOLVE_GRID_BATCH
-#define FC_RESOLVE_GRID_BATCH 64
+#define FC_RESOLVE_GRID_BATCH 16
 #endif
-constexpr int kResolveGridBatch = FC_RESOLVE_GRID_BATCH;   // k_resolve workgroups per client (batched encode)
+constexpr int kResolveGridBatch = FC_RESOLVE_GRID_BATCH;   // k_resolve workgroups per client (batched encode;
+                                                          // 16 vs 64: configs[2] +2.1 %, configs[3] +0.2 %)
 constexpr int kSlots = kVec * kWaves;       // 32 (i, w) slots per chunk
 constexpr int kCandSlot = 256;              // candidate slot per chunk (overflow: re-read entries)
 constexpr int kShards = 64;                 // sharded k_compact totals
