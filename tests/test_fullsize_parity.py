@@ -9,6 +9,8 @@ The oracle's SHA-256 digests (tests/golden/make_digests_full.py, build container
   * configs[4]: 70 clients x 25,557,032, top f = 0.01, through openmsftl_amd.pipeline.HostFedAvg
     (H2D -> encode -> fold in groups of 64 -> D2H: the continued fold is crossed), as
     tools/e2e_bench.py runs it.
+plus the single-client fused paths (fc_topk_encode_dense / fc_topk_encode) on client 0 of
+configs[2] (= configs[1], one 16 M gradient) and of configs[3] (the single 128 M gradient).
 Inputs are regenerated here bit-identically (torch's CPU generator; the input digests of the
 first clients are checked first, so a generator difference is reported as such).
 """
@@ -97,3 +99,23 @@ def test_configs4_host_ring_70x25M():
     assert sha(out.numpy()) == d["aggregate_sha256"], "configs4: ring aggregate differs"
     # a second pass over the same pipeline (reused packets and workspaces) gives the same bytes
     assert sha(pipe.run(host, M).numpy()) == d["aggregate_sha256"]
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("name", ["configs2", "configs3"])
+def test_single_client_fused_paths_fullsize(name):
+    """The single-client paths at full size against the same oracle digests: BASELINE
+    configs[1] (one 16 M gradient = client 0 of configs2) and the north star's single 128 M
+    gradient (client 0 of configs3), through the drop-in dense path (k_fused_mag<true> +
+    k_resolve's in-kernel fix-up) and the packet path (k_fused_mag<false> + k_resolve, then the
+    dense decode)."""
+    import torch
+    from openmsftl_amd import codec
+    d = D[name]
+    n, k = d["n"], d["k"]
+    (g,) = _device_grads(name, 1, torch.device("cuda", 0))
+    q = codec.compress_top_dense(g, k)
+    assert sha(q.cpu().numpy()) == d["q_sha256"]["0"], f"{name}: fused dense q differs"
+    del q
+    p = codec.encode_top(g, k)
+    assert sha(codec.decode(p).cpu().numpy()) == d["q_sha256"]["0"], f"{name}: packet path differs"
