@@ -806,9 +806,10 @@ __global__ __launch_bounds__(kQBlock, 4) void k_fold_q(DecodeArgs a) {
         const uint32_t ib = uni32(pm.flags) & 0xffu;
         const uint32_t st = st_[sl][d], en = en_[sl][d];
         // slack filter comp >= T64 (T64 = 0 keeps every entry: comp >= 0).  Measured slower:
-        // a per-item float threshold |v| !< Tf behind a uniform exact/fast branch (+4 %) and
-        // skipping the rounds past the item's count (+27 %): control flow inside the unrolled
-        // group costs more than the VALU it saves.
+        // a per-item float threshold |v| !< Tf behind a uniform exact/fast branch (+4 %),
+        // skipping the rounds past the item's count (+27 %) — control flow inside the unrolled
+        // group costs more than the VALU it saves — and one no-return ds_add_f32 per entry
+        // instead of the read + write (bit-exact, but 3.7x slower).
         const uint32_t b32 = (uint32_t)base;
         uint32_t loc[kQR];
         bool ok[kQR];
