@@ -147,19 +147,35 @@ def cpu_matrix(n16=16_777_216, n25=25_557_032):
             "cores": 1, "kind": "port (the reference's NumPy calls; default argsort kind)"}
 
 
+def _packet_equal(torch, p, q):
+    """Byte equality of two packets on the device: every listed entry (idx, val), the slot
+    counts, quarter offsets and header fields thresh / lower / n_entries / status."""
+    if not (torch.equal(p.cnt, q.cnt) and torch.equal(p.qoff, q.qoff)):
+        return False
+    hp, hq = p.hdr.view(torch.int64)[:3], q.hdr.view(torch.int64)[:3]   # thresh, lower, n|k
+    if not (torch.equal(hp, hq) and torch.equal(p.hdr[36:40], q.hdr[36:40])):  # + status
+        return False
+    pos = torch.arange(p.capacity, device=p.val.device)
+    listed = (pos % 8192) < p.cnt.to(torch.int64)[pos // 8192]
+    return bool(torch.equal(p.idx[listed], q.idx[listed])
+                and torch.equal(p.val.view(torch.int32)[listed], q.val.view(torch.int32)[listed]))
+
+
 def self_check(torch, codec, grads, pkts, k):
     """Outside the timed region: clients 0 and 1 re-encoded ALONE (fc_topk_encode) give the
-    batched packets' dense result bit for bit (compression.py:31-37 per client)."""
+    batched packets byte for byte, and the same dense result (compression.py:31-37)."""
     ok = True
     for i in (0, 1):
         single = codec.encode_top(grads[i], k)
+        ok = ok and _packet_equal(torch, single, pkts[i])
         a = codec.decode(single).view(torch.int32)
         b = codec.decode(pkts[i]).view(torch.int32)
         ok = ok and bool(torch.equal(a, b))
         del single, a, b
     if not ok:
         raise SystemExit("self-check failed: batched encode differs from a single-client encode")
-    return "ok: clients 0, 1 re-encoded singly, dense results bit-identical to the batch"
+    return ("ok: clients 0, 1 re-encoded singly: packets byte-equal to the batch's (entries, "
+            "counts, quarter offsets, header) and dense results bit-identical")
 
 
 def load_pmc(path):

@@ -263,7 +263,6 @@ __device__ __forceinline__ void sample_body(const float* __restrict__ g, const S
     }
   }
   for (int b = tid; b < kHistBins; b += kBlock) h[b] = 0;
-  if (bid == 0 && tid == 0) write_hdr_static(hdr, HI);
   FineWin F;
   if (!shared_pilot || bid == 0) {
     F = pilot_window<KM>(g, P, seed, off, h, s_tmp, s_out, bid == 0, xs, es, ls);
@@ -343,6 +342,9 @@ __device__ __forceinline__ void sample_body(const float* __restrict__ g, const S
     S->n_cand = 0; S->cand_over = 0; S->ent_over = 0;
     S->win_flag = 0;               // (err: set by a timed-out wait, read and
                                                   // cleared by this call's k_resolve)
+    // the header's only writer in this launch: a static header written by workgroup 0 at its
+    // start raced this store through another XCD's L2 (lower read back as 0)
+    write_hdr_static(hdr, HI);
     hdr->lower = (uint64_t)t_lo << ib;
     if (pub) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -63,6 +63,12 @@ def _check_top_packet(g_np, k, pkt, out):
     np.testing.assert_array_equal(idx[kept], want_idx)
     assert val.tobytes() == g_np[idx].tobytes()
     assert h.n_entries >= k and kept.sum() == k
+    # L64 (header `lower`): every listed entry has comp >= L64 and L64 <= T64; the sample's
+    # last workgroup is the header's only writer (a second writer once left it at 0)
+    assert np.uint64(h.lower) <= np.uint64(h.thresh)
+    assert len(c) == 0 or c.min() >= np.uint64(h.lower)
+    if k and h.n_entries > k:                      # slack listed: the bracket's lower end is set
+        assert h.lower > 0 or po.comps(keys).min() == 0
 
 
 # ---- top: golden cases ----------------------------------------------------------------
