@@ -41,7 +41,7 @@ ENTRY_BYTES = 8.0
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=300)   # ~5.3 s timed: visible to a 5-s GPU-busy sampler
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--clients", type=int, default=128, help="clients per GPU")
     ap.add_argument("--n", type=int, default=134_217_728, help="gradient length (fp32)")
