@@ -648,14 +648,23 @@ __global__ __launch_bounds__(kSBlock, kSBlocksPerCU) void k_decode_sparse(Decode
 constexpr int kQBlock = 256;
 constexpr int kQuarter = kChunk / 4;
 #ifndef FC_QR
-#define FC_QR 5
+#define FC_QR 4
 #endif
-constexpr int kQR = FC_QR;                      // entry rounds (x64 lanes) loaded per item: 320
-                                                // entries, ~8 sigma above a quarter at f = 0.1
+constexpr int kQR = FC_QR;                      // entry rounds (x64 lanes) loaded per item: 256
+                                                // entries (a quarter holds ~205 at f = 0.1; the
+                                                // rare longer item folds its rest in a tail
+                                                // loop: 4 rounds + tail 17.7 us/packet against
+                                                // 5 rounds 19.9, 5 + tail 18.6)
 #ifndef FC_QG
 #define FC_QG 3
 #endif
 constexpr int kQGroup = FC_QG;                  // items per load group
+#ifndef FC_QTAIL
+#define FC_QTAIL 8
+#endif
+// FC_QTAIL > kQR: an item holding more than kQR * 64 entries folds the rest in a tail loop
+// right after its rounds; only a quarter above FC_QTAIL * 64 entries takes the slow body
+constexpr int kQTail = FC_QTAIL > FC_QR ? FC_QTAIL : FC_QR;
 
 struct QMeta {
   const void* idx;                              // uint16 chunk-local indices
@@ -721,7 +730,7 @@ __global__ __launch_bounds__(kQBlock, 4) void k_fold_q(DecodeArgs a) {
     const uint32_t en = q == 3 ? (uint32_t)(v >> 48) : (uint32_t)(v >> (16 * q)) & 0xffffu;
     return en - st;
   };
-  const bool dense_q = __any(qcount(qo0) > (uint32_t)(kQR * 64) || qcount(qo1) > (uint32_t)(kQR * 64));
+  const bool dense_q = __any(qcount(qo0) > (uint32_t)(kQTail * 64) || qcount(qo1) > (uint32_t)(kQTail * 64));
   auto range = [&](uint32_t m, uint32_t& st, uint32_t& en) {   // uniform
     const uint64_t src = m < 64 ? qo0 : qo1;
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)src, (int)(m & 63));
@@ -826,6 +835,17 @@ __global__ __launch_bounds__(kQBlock, 4) void k_fold_q(DecodeArgs a) {
 #pragma unroll
         for (int r = 0; r < kQR; ++r)
           if (ok[r]) qt[loc[r]] = __fadd_rn(tv[r], __fmul_rn(vs_[sl][d][r], w));
+        if (kQTail > kQR && en - st > (uint32_t)(kQR * 64)) {      // rare, uniform: the rest
+          gf32* val = (gf32*)uni_ptr(pm.val) + base;
+          gu16* idx = (gu16*)uni_ptr(pm.idx) + base;
+          for (uint32_t e = st + (uint32_t)(kQR * 64) + lane; e < en; e += 64) {
+            const uint32_t lc = idx[e];
+            const float v = val[e];
+            const uint32_t l2 = lc - (uint32_t)(q * kQuarter);
+            if (l2 < (uint32_t)kQuarter && comp_of(mag_key(v), b32 + lc, ib) >= thresh)
+              qt[l2] = __fadd_rn(qt[l2], __fmul_rn(v, w));
+          }
+        }
       }
     };
     issue(0, 0);
