@@ -708,10 +708,10 @@ template <int STAGE, bool RAWBAR>
 struct MagSharedT {
   static constexpr int kStageN = STAGE;
   uint32_t gcnt[kMGroups / 4];                     // 4 group counts (bytes, <= 64) per (i, w)
-  uint32_t ncand[2];                               // candidates appended (by item parity)
-  uint32_t pad_[2];
+  uint32_t wcnt[8];                                // candidates per wave (may exceed its sub-slot)
   uint2 st[STAGE + 4];                             // packed {chunk-local index, value bits}
-  uint16_t cbin[STAGE + 2];
+  uint64_t cst[kCandSlot];                         // candidate comps: wave w's sub-slot at w * kCW
+  uint16_t cstb[kCandSlot];                        // their candidate-histogram bins
   __device__ static void barrier() {
     if (RAWBAR) lds_barrier();
     else __syncthreads();
@@ -774,7 +774,7 @@ struct MagOut {
 template <bool FAST, typename SH, int NW, bool DENSE = false>
 __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred& P,
                                                  float (&x)[MagGeo<NW>::kQ], SH& sh,
-                                                 uint32_t chunk, uint32_t sbin, uint32_t par) {
+                                                 uint32_t chunk, uint32_t sbin) {
   const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
   const uint32_t base = chunk * (uint32_t)kChunk;
   const uint32_t lbase = (uint32_t)(w * 256 + lane);
@@ -799,8 +799,6 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
   // live in SGPRs across the scan (that spilled 87 SGPRs)
 #pragma unroll
   for (int q = 0; q < NQ; ++q) asm volatile("" : "+v"(x[q]));
-  // the other parity's counter was last read before this item's barrier: reset it for the next
-  if (tid == 0) sh.ncand[par ^ 1u] = 0;
   // every wave scans the 32 packed (i, w) words itself (no second barrier): lane L < 32 holds
   // word L = (i, w), in element order
   const uint32_t word = lane < kMGroups / 4 ? sh.gcnt[lane] : 0u;
@@ -854,36 +852,53 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
       dense_out(q, p);
     }
   }
-  // ---- candidates (rare; wave-uniform skip per group) ------------------------------------
+  // ---- candidates (key in [t_lo, t_hi]): wave w stages them in its own LDS sub-slot of kCW
+  // at a wave-uniform running count: no atomic and no branch per group (a per-group LDS atomic
+  // reservation cost ~14 % of the compaction at 16 M).  Past kCW, a wave bins the rest straight
+  // into chist and the chunk is marked overflowed (the resolve re-reads its entries slot). ----
+  constexpr int kCW = kCandSlot / NW;
+  uint32_t wc = 0;
+#ifdef FC_ABL_CAND                                    // timing-only ablation (wrong results)
+  if (false) {
+#else
   if (P.cand_on) {
-    const uint64_t cslot = (uint64_t)chunk * kCandSlot;
+#endif
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const bool c = mag_cand<FAST>(P, x[q]);
       const uint64_t mc = __ballot(c);
-      if (mc) {                                    // wave-uniform
-        uint32_t b0 = 0;
-        if (lane == 0) b0 = atomicAdd(&sh.ncand[par], (uint32_t)__popcll(mc));
-        const uint32_t cpos = (uint32_t)__builtin_amdgcn_readfirstlane((int)b0) + prefix_count(mc);
-        if (c) {
-          const uint32_t e = base + FC_LOC(q);
-          const uint32_t key = mag_key(FAST ? x[q] : a.g[e]);
-          if (cpos < (uint32_t)kCandSlot) a.cand[cslot + cpos] = comp_of(key, e, a.ib);
-          const uint32_t bin = (key - P.t_lo) >> sbin;
-          if (cpos < (uint32_t)SH::kStageN) sh.cbin[cpos] = (uint16_t)bin;
-          else atomicAdd(&a.chist[bin], 1u);
+      const uint32_t pos = wc + prefix_count(mc);
+      if (c) {
+        const uint32_t e = base + FC_LOC(q);
+        const uint32_t key = mag_key(FAST ? x[q] : a.g[e]);
+        const uint32_t bin = (key - P.t_lo) >> sbin;
+        if (pos < (uint32_t)kCW) {
+          sh.cst[w * kCW + pos] = comp_of(key, e, a.ib);
+          sh.cstb[w * kCW + pos] = (uint16_t)bin;
+        } else {
+          atomicAdd(&a.chist[bin], 1u);
         }
       }
+      wc += (uint32_t)__popcll(mc);
     }
   }
+  if (lane == 0) sh.wcnt[w] = wc;
 #undef FC_LOC
   SH::barrier();
-  const uint32_t tot_c = sh.ncand[par];
+  uint32_t wn[NW], tot_c = 0;
+  bool c_ovf = false;
+#pragma unroll
+  for (int j = 0; j < NW; ++j) {
+    wn[j] = sh.wcnt[j];
+    tot_c += wn[j];
+    c_ovf |= wn[j] > (uint32_t)kCW;
+  }
   if (tid == 0) {
     TopkState* S = a.S;
     a.cnt[chunk] = tot_e;
     if (a.qoff) a.qoff[chunk] = qs1 | ((uint64_t)qs2 << 16) | ((uint64_t)qs3 << 32) | ((uint64_t)tot_e << 48);
-    a.ccnt[chunk] = tot_c;
+    // a wave past its sub-slot: report more than the slot holds (k_resolve's overflow test)
+    a.ccnt[chunk] = c_ovf ? max(tot_c, (uint32_t)kCandSlot + 1u) : tot_c;
     atomicAdd(&S->shard_ent[chunk % kShards], tot_e);
     if (tot_c) atomicAdd(&S->shard_cnd[chunk % kShards], tot_c);
   }
@@ -903,8 +918,26 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
       }
     }
   }
-  const uint32_t nb = tot_c < (uint32_t)SH::kStageN ? tot_c : (uint32_t)SH::kStageN;
-  for (uint32_t t = tid; t < nb; t += MagGeo<NW>::kThreads) atomicAdd(&a.chist[sh.cbin[t]], 1u);
+  // staged candidates out: thread t < kCandSlot holds sub-slot entry (t / kCW, t % kCW); its
+  // place in the chunk's candidate slot is the wave-major prefix
+  if (tot_c && tid < kCandSlot) {
+    const uint32_t wj = (uint32_t)tid / kCW, p = (uint32_t)tid % kCW;
+    uint32_t pre = 0, nj = 0;
+#pragma unroll
+    for (int j = 0; j < NW; ++j) {
+      const uint32_t m = min(wn[j], (uint32_t)kCW);
+      if ((uint32_t)j < wj) pre += m;
+      if ((uint32_t)j == wj) nj = m;
+    }
+    if (p < nj) {
+#ifndef FC_ABL_CHIST
+      atomicAdd(&a.chist[sh.cstb[tid]], 1u);
+#endif
+#ifndef FC_ABL_COUT
+      if (!c_ovf) a.cand[(uint64_t)chunk * kCandSlot + pre + p] = sh.cst[tid];
+#endif
+    }
+  }
 }
 
 // Per-client records (job table, encoder state) are read with SCALAR loads: no kernel of this
@@ -1003,7 +1036,7 @@ __device__ __forceinline__ void mag_load(const float* g, uint32_t chunk, uint64_
 template <int NW, typename SH, bool DENSE = false>
 __device__ __forceinline__ void compact_mag_item(const CompactArgs& a0, const MagOut& o,
                                                  uint32_t chunk, const MagState& st,
-                                                 float (&x)[MagGeo<NW>::kQ], SH& sh, uint32_t par) {
+                                                 float (&x)[MagGeo<NW>::kQ], SH& sh) {
   const int tid = threadIdx.x;
   const uint32_t base = chunk * (uint32_t)kChunk;
   const bool full = (uint64_t)base + kChunk <= a0.n;
@@ -1022,7 +1055,7 @@ __device__ __forceinline__ void compact_mag_item(const CompactArgs& a0, const Ma
   P.cand_all = P.t_hi >= 0x7f800001u;
   P.T_hi = __uint_as_float(P.cand_all ? 0x7f800000u : P.t_hi);
   if (fast) {
-    compact_mag_body<true, SH, NW, DENSE>(o, P, x, sh, chunk, st.sbin, par);
+    compact_mag_body<true, SH, NW, DENSE>(o, P, x, sh, chunk, st.sbin);
   } else if (none) {                                       // k = 0: nothing listed
     SH::barrier();
     if (tid == 0) {
@@ -1035,7 +1068,7 @@ __device__ __forceinline__ void compact_mag_item(const CompactArgs& a0, const Ma
         o.dense[base + i] = 0.0f;
   } else {                                                 // rare: exact integer predicate
     mag_exact_bits<NW>(P, x, base + (uint32_t)((tid >> 6) * 256 + lane_id()));
-    compact_mag_body<false, SH, NW, DENSE>(o, P, x, sh, chunk, st.sbin, par);
+    compact_mag_body<false, SH, NW, DENSE>(o, P, x, sh, chunk, st.sbin);
   }
 }
 
@@ -1083,8 +1116,7 @@ __device__ __forceinline__ void compact_mag_wg(const CompactArgs& a0) {
   float x[MagGeo<NW>::kQ];
   mag_load<NW>(mag_g(a0, client), chunk, a0.n, x);       // g first, state behind it
   const MagState st = mag_state(mag_S(a0, client));
-  if (threadIdx.x == 0) sh.ncand[0] = 0;
-  compact_mag_item<NW, MagShared, DENSE>(a0, mag_out(a0, client), chunk, st, x, sh, 0u);
+  compact_mag_item<NW, MagShared, DENSE>(a0, mag_out(a0, client), chunk, st, x, sh);
 }
 // 512 threads (8 waves x 16 elements per lane)
 __global__ __launch_bounds__(kCBlock, FC_MAG1_WAVES_PER_EU) void k_compact_mag1(CompactArgs a0) {
@@ -1139,12 +1171,11 @@ __global__ __launch_bounds__(kCBlock, FC_MAG1_WAVES_PER_EU) void k_fused_mag(Com
     m.t_lo = ld_agent(&S->t_lo); m.t_hi = ld_agent(&S->t_hi);
     m.cand_on = ld_agent(&S->cand_on); m.sbin = ld_agent(&S->sbin);
     s_st = m;
-    u.m.ncand[0] = 0;
   }
   __syncthreads();
   FC_TR(25);
   const MagState st = s_st;
-  compact_mag_item<8, MagShared, DENSE>(a0, mag_out(a0, 0u), chunk, st, x, u.m, 0u);
+  compact_mag_item<8, MagShared, DENSE>(a0, mag_out(a0, 0u), chunk, st, x, u.m);
   FC_TR(26);
 }
 template __global__ void k_fused_mag<false>(CompactArgs, SamplePlan, HdrInit, uint32_t);

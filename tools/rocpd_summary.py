@@ -5,6 +5,7 @@
         [--alg-bytes B] [--calib profiles/<tag>_pmc_calib.json]
     python tools/rocpd_summary.py calib <fetch.db> <write.db> <out.json>
     python tools/rocpd_summary.py counters <db> <kernel-substring>
+    python tools/rocpd_summary.py timeline <db> [last-N-dispatches]
 
 `stats` is the per-kernel table rocprofv3 --stats prints (calls, total/avg/min/max ns, %).
 `pmc` averages FETCH_SIZE / WRITE_SIZE (kilobytes, one --pmc pass each) over the dispatches of
@@ -35,6 +36,24 @@ def kernel_rows(db):
         return [(f"{n} [grid {x}x{y}]", d) for n, d, x, y in
                 c.execute(f"select name, duration, {gx}, {gy} from kernels")]
     return c.execute("select name, duration from kernels").fetchall()
+
+
+def timeline(db, last=60):
+    """The last dispatches in start order: start / end (us, relative to the first shown),
+    duration and name (with grid), to see how launches of different streams overlap."""
+    c = sqlite3.connect(db)
+    cols = [r[1] for r in c.execute("pragma table_info(kernels)")]
+    st = next(x for x in ("start", "start_ns", "begin") if x in cols)
+    en = next(x for x in ("end", "end_ns") if x in cols)
+    gx = next((x for x in ("grid_size_x", "grid_x") if x in cols), None)
+    gy = next((x for x in ("grid_size_y", "grid_y") if x in cols), None)
+    q = f"select name, {st}, {en}" + (f", {gx}, {gy}" if gx and gy else "") + f" from kernels order by {st}"
+    rows = [r for r in c.execute(q).fetchall() if "fc::" in r[0]][-last:]
+    t0 = rows[0][1]
+    for r in rows:
+        grid = f" [grid {r[3]}x{r[4]}]" if len(r) > 3 else ""
+        print(f"{(r[1] - t0) / 1e3:10.1f} {(r[2] - t0) / 1e3:10.1f} {(r[2] - r[1]) / 1e3:9.1f}  "
+              f"{r[0][:70]}{grid}")
 
 
 def stats(db, out):
@@ -137,6 +156,9 @@ def main():
     k = sub.add_parser("counters")
     k.add_argument("db")
     k.add_argument("kernel")
+    t = sub.add_parser("timeline")
+    t.add_argument("db")
+    t.add_argument("last", type=int, nargs="?", default=60)
     c = sub.add_parser("calib")
     c.add_argument("fetch_db")
     c.add_argument("write_db")
@@ -145,6 +167,8 @@ def main():
     if a.cmd == "stats":
         for name, d in stats(a.db, a.out)[:12]:
             print(f"{len(d):7d} {sum(d) / len(d) / 1e3:10.2f} us  {name[:100]}")
+    elif a.cmd == "timeline":
+        timeline(a.db, a.last)
     elif a.cmd == "counters":
         print(json.dumps(counters(a.db, a.kernel), indent=1))
     elif a.cmd == "calib":
