@@ -350,6 +350,7 @@ int fc_topk_encode(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_
   if (rc) return rc;
   rc = launch_compact_key(key_mode, ca, s);
   if (rc) return rc;
+  ra.rbin = 1;                       // k_compact / k_compact_mag1 leave the binning to k_resolve
   return launch_resolve(ra, s);
 }
 
@@ -371,6 +372,7 @@ int fc_topk_encode_dense(const float* g, uint64_t n, uint64_t k, uint16_t* idx, 
     rc = launch_fused(ca, P, hi, sgrid, s);
     if (rc) return rc;
   } else {
+    ra.rbin = 1;
     rc = launch_sample(FC_KEY_MAGNITUDE, dim3(sgrid), g, P, 0ull, 0ull, ca.W, ca.ib, hdr, hi, nullptr, 0ull, s);
     if (rc) return rc;
     TimedLaunch t(FC_TIME_COMPACT, s);
@@ -424,6 +426,7 @@ int fc_topk_encode_batch_part(const fc_encode_job* jobs, int m, uint64_t n, uint
   memset(&ra, 0, sizeof ra);
   ra.ib = ib; ra.nchunks = ca.nchunks; ra.k = k; ra.key_mode = (uint32_t)key_mode;
   ra.W = ca.W; ra.jobs = jobs; ra.ws_stride = stride;
+  ra.rbin = 1;                       // batched compaction: k_resolve bins the candidates
   hipStream_t s = (hipStream_t)stream;
   const SamplePlan P = make_plan(n, k);
   const dim3 sgrid((P.nseg + kSampleSegs - 1) / kSampleSegs, (uint32_t)m);

@@ -27,6 +27,8 @@ struct alignas(16) TopkState {
   uint32_t gen;          // k_resolve generation: bumped when T64 is published (dense fix-up)
   uint32_t fz_pub;       // k_fused_mag: the bracket is written (= fz_seq + 1 of that launch)
   uint32_t fz_seq;       // k_fused_mag launches completed (bumped by the following k_resolve)
+  uint32_t hgen;         // k_resolve: bumped once the bin beta below is published
+  uint32_t rb_beta, rb_rin, rb_cnt;   // k_resolve: bin holding rank r, rank inside it, its count
   uint32_t pad_[3];
   uint32_t shard_ent[kShards];   // k_compact totals, 64-way sharded (no hot word)
   uint32_t shard_cnd[kShards];
@@ -34,6 +36,7 @@ struct alignas(16) TopkState {
 static_assert(sizeof(TopkState) <= 1024, "state block");
 
 constexpr int kSampleShards = 8;            // k_sample1's global histogram, sharded by workgroup
+constexpr int kCandShards = 8;              // k_resolve's candidate histogram, likewise
 constexpr int kTickGroups = 16;             // two-level last-arriver tickets (fc_common.h)
 constexpr int kTickStride = 64;             // u32 per ticket counter (one 256-B line each)
 constexpr int kTickWords = (kTickGroups + 1) * kTickStride;
@@ -47,9 +50,9 @@ struct WsLayout {
     L.cand_cap = L.nchunks * kCandSlot;                // per-chunk candidate slots
     uint64_t o = 1024;
     L.off_hist1 = o;  o += 4ull * kHistBins * kSampleShards;
-    L.off_tick = o;   o += 4ull * kTickWords * 2;      // sample ticket, resolve ticket
+    L.off_tick = o;   o += 4ull * kTickWords * 3;      // sample, resolve (gather), resolve (bins)
     L.off_ehist = o;  o += 4ull * kHistBins;
-    L.off_chist = o;  o += 4ull * kHistBins;
+    L.off_chist = o;  o += 4ull * kHistBins * kCandShards;
     L.off_small = o;  o += 8ull * kSmallCap;
     L.off_status = o; o += 4ull * (L.nchunks ? L.nchunks : 1);   // per-chunk candidate counts
     o = (o + 15) & ~15ull;
@@ -67,7 +70,7 @@ struct HdrInit {          // static header fields, written by the first kernel o
 
 struct WsPtrs {
   TopkState* st;
-  uint32_t *hist1, *tick, *ehist, *chist;   // hist1: kSampleShards x 4096; tick: 2 tickets
+  uint32_t *hist1, *tick, *ehist, *chist;   // hist1: kSampleShards x 4096; tick: 3 tickets
   uint64_t* small;
   uint32_t* ccnt;          // candidates per chunk (may exceed kCandSlot: overflowed chunk)
   uint64_t* cand;          // chunk c's candidates at [c * kCandSlot, + min(ccnt, kCandSlot))

@@ -457,7 +457,6 @@ __global__ __launch_bounds__(kCBlock, FC_COMPACT_WAVES_PER_EU) void k_compact(Co
   // nothing left to write in a round store to their own dummy slot kStage + lane (one shared
   // dummy made every store a ~58-way LDS bank conflict — measured 65 us of a 165 us launch)
   __shared__ __attribute__((aligned(16))) uint2 st[kStage + 64];
-  __shared__ uint16_t s_cbin[PRED == kPredKey ? kStage + 2 : 2];
   const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
   TopkState* S = a.W.st;
   const uint32_t chunk = blockIdx.x;
@@ -478,13 +477,13 @@ __global__ __launch_bounds__(kCBlock, FC_COMPACT_WAVES_PER_EU) void k_compact(Co
   }
 
   uint32_t Lk = 0;   // key part of L64; 0xffffffff (above every key) selects nothing
-  uint32_t Li = 0, t_lo = 0, t_hi = 0xffffffffu, cand_on = 0, sbin = 0;
+  uint32_t Li = 0, t_lo = 0, t_hi = 0xffffffffu, cand_on = 0;
   if (PRED == kPredKey) {
     const uint64_t L64 = S->L64;
     const bool none = L64 == kSelectNothing;
     Lk = none ? 0xffffffffu : (uint32_t)(L64 >> a.ib);
     Li = none ? 0xffffffffu : (uint32_t)(L64 & ((1ull << a.ib) - 1));
-    t_lo = S->t_lo; t_hi = S->t_hi; cand_on = S->cand_on; sbin = S->sbin;
+    t_lo = S->t_lo; t_hi = S->t_hi; cand_on = S->cand_on;
   }
 
   // ---- predicates (branchless): bit (i*4 + j) -------------------------------------------
@@ -638,9 +637,6 @@ __global__ __launch_bounds__(kCBlock, FC_COMPACT_WAVES_PER_EU) void k_compact(Co
           asm volatile("" : "+v"(xv), "+v"(e));
           const uint32_t key = key1<KM>(xv, e, a.seed, a.offset);
           if (cpos < (uint32_t)kCandSlot) a.W.cand[cslot + cpos] = comp_of(key, e, a.ib);
-          const uint32_t bin = (key - t_lo) >> sbin;
-          if (cpos < (uint32_t)kStage) s_cbin[cpos] = (uint16_t)bin;
-          else atomicAdd(&a.W.chist[bin], 1u);
           ++cpos;
         }
       }
@@ -663,11 +659,6 @@ __global__ __launch_bounds__(kCBlock, FC_COMPACT_WAVES_PER_EU) void k_compact(Co
         }
       }
     }
-  }
-  if (PRED == kPredKey) {
-    const uint32_t tot_c = s_tot[1];
-    const uint32_t nb = tot_c < (uint32_t)kStage ? tot_c : (uint32_t)kStage;
-    for (uint32_t t = tid; t < nb; t += kCBlock) atomicAdd(&a.W.chist[s_cbin[t]], 1u);
   }
 }
 
@@ -711,7 +702,7 @@ struct MagSharedT {
   uint32_t wcnt[8];                                // candidates per wave (may exceed its sub-slot)
   uint2 st[STAGE + 4];                             // packed {chunk-local index, value bits}
   uint64_t cst[kCandSlot];                         // candidate comps: wave w's sub-slot at w * kCW
-  uint16_t cstb[kCandSlot];                        // their candidate-histogram bins
+  uint16_t cstb[kCandSlot];                        // their candidate-histogram bins (BIN)
   __device__ static void barrier() {
     if (RAWBAR) lds_barrier();
     else __syncthreads();
@@ -771,7 +762,7 @@ struct MagOut {
   float* dense;             // nullptr unless fc_topk_encode_dense
 };
 
-template <bool FAST, typename SH, int NW, bool DENSE = false>
+template <bool FAST, typename SH, int NW, bool DENSE, bool BIN>
 __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred& P,
                                                  float (&x)[MagGeo<NW>::kQ], SH& sh,
                                                  uint32_t chunk, uint32_t sbin) {
@@ -854,8 +845,12 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
   }
   // ---- candidates (key in [t_lo, t_hi]): wave w stages them in its own LDS sub-slot of kCW
   // at a wave-uniform running count: no atomic and no branch per group (a per-group LDS atomic
-  // reservation cost ~14 % of the compaction at 16 M).  Past kCW, a wave bins the rest straight
-  // into chist and the chunk is marked overflowed (the resolve re-reads its entries slot). ----
+  // reservation cost ~14 % of the compaction at 16 M).  A wave past kCW marks the chunk
+  // overflowed (the resolve re-reads its entries slot).  BIN (a lone client's fused launch):
+  // the candidates also go into the candidate histogram, one global atomic each; batched
+  // launches leave that to k_resolve, which reads them anyway (the atomics cost 5.7 % of this
+  // pass at 128 M; the resolve's own binning adds a grid barrier, hidden behind the other
+  // encode chain but not on a lone client's critical path).
   constexpr int kCW = kCandSlot / NW;
   uint32_t wc = 0;
 #ifdef FC_ABL_CAND                                    // timing-only ablation (wrong results)
@@ -871,12 +866,11 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
       if (c) {
         const uint32_t e = base + FC_LOC(q);
         const uint32_t key = mag_key(FAST ? x[q] : a.g[e]);
-        const uint32_t bin = (key - P.t_lo) >> sbin;
-        if (pos < (uint32_t)kCW) {
-          sh.cst[w * kCW + pos] = comp_of(key, e, a.ib);
-          sh.cstb[w * kCW + pos] = (uint16_t)bin;
-        } else {
-          atomicAdd(&a.chist[bin], 1u);
+        if (pos < (uint32_t)kCW) sh.cst[w * kCW + pos] = comp_of(key, e, a.ib);
+        if (BIN) {
+          const uint32_t bin = (key - P.t_lo) >> sbin;
+          if (pos < (uint32_t)kCW) sh.cstb[w * kCW + pos] = (uint16_t)bin;
+          else atomicAdd(&a.chist[bin], 1u);
         }
       }
       wc += (uint32_t)__popcll(mc);
@@ -920,7 +914,7 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
   }
   // staged candidates out: thread t < kCandSlot holds sub-slot entry (t / kCW, t % kCW); its
   // place in the chunk's candidate slot is the wave-major prefix
-  if (tot_c && tid < kCandSlot) {
+  if (tot_c && (BIN || !c_ovf) && tid < kCandSlot) {
     const uint32_t wj = (uint32_t)tid / kCW, p = (uint32_t)tid % kCW;
     uint32_t pre = 0, nj = 0;
 #pragma unroll
@@ -930,12 +924,8 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
       if ((uint32_t)j == wj) nj = m;
     }
     if (p < nj) {
-#ifndef FC_ABL_CHIST
-      atomicAdd(&a.chist[sh.cstb[tid]], 1u);
-#endif
-#ifndef FC_ABL_COUT
+      if (BIN) atomicAdd(&a.chist[sh.cstb[tid]], 1u);
       if (!c_ovf) a.cand[(uint64_t)chunk * kCandSlot + pre + p] = sh.cst[tid];
-#endif
     }
   }
 }
@@ -1033,7 +1023,7 @@ __device__ __forceinline__ void mag_load(const float* g, uint32_t chunk, uint64_
 // workgroups per CU overlap one another's load latency.  (A persistent variant that kept the
 // next item's loads in flight measured 1.3-2.5x SLOWER: hipcc spilled the second register set
 // and loop-carried state)
-template <int NW, typename SH, bool DENSE = false>
+template <int NW, typename SH, bool DENSE, bool BIN>
 __device__ __forceinline__ void compact_mag_item(const CompactArgs& a0, const MagOut& o,
                                                  uint32_t chunk, const MagState& st,
                                                  float (&x)[MagGeo<NW>::kQ], SH& sh) {
@@ -1055,7 +1045,7 @@ __device__ __forceinline__ void compact_mag_item(const CompactArgs& a0, const Ma
   P.cand_all = P.t_hi >= 0x7f800001u;
   P.T_hi = __uint_as_float(P.cand_all ? 0x7f800000u : P.t_hi);
   if (fast) {
-    compact_mag_body<true, SH, NW, DENSE>(o, P, x, sh, chunk, st.sbin);
+    compact_mag_body<true, SH, NW, DENSE, BIN>(o, P, x, sh, chunk, st.sbin);
   } else if (none) {                                       // k = 0: nothing listed
     SH::barrier();
     if (tid == 0) {
@@ -1068,7 +1058,7 @@ __device__ __forceinline__ void compact_mag_item(const CompactArgs& a0, const Ma
         o.dense[base + i] = 0.0f;
   } else {                                                 // rare: exact integer predicate
     mag_exact_bits<NW>(P, x, base + (uint32_t)((tid >> 6) * 256 + lane_id()));
-    compact_mag_body<false, SH, NW, DENSE>(o, P, x, sh, chunk, st.sbin);
+    compact_mag_body<false, SH, NW, DENSE, BIN>(o, P, x, sh, chunk, st.sbin);
   }
 }
 
@@ -1116,7 +1106,7 @@ __device__ __forceinline__ void compact_mag_wg(const CompactArgs& a0) {
   float x[MagGeo<NW>::kQ];
   mag_load<NW>(mag_g(a0, client), chunk, a0.n, x);       // g first, state behind it
   const MagState st = mag_state(mag_S(a0, client));
-  compact_mag_item<NW, MagShared, DENSE>(a0, mag_out(a0, client), chunk, st, x, sh);
+  compact_mag_item<NW, MagShared, DENSE, false>(a0, mag_out(a0, client), chunk, st, x, sh);
 }
 // 512 threads (8 waves x 16 elements per lane)
 __global__ __launch_bounds__(kCBlock, FC_MAG1_WAVES_PER_EU) void k_compact_mag1(CompactArgs a0) {
@@ -1175,7 +1165,7 @@ __global__ __launch_bounds__(kCBlock, FC_MAG1_WAVES_PER_EU) void k_fused_mag(Com
   __syncthreads();
   FC_TR(25);
   const MagState st = s_st;
-  compact_mag_item<8, MagShared, DENSE>(a0, mag_out(a0, 0u), chunk, st, x, u.m);
+  compact_mag_item<8, MagShared, DENSE, true>(a0, mag_out(a0, 0u), chunk, st, x, u.m);
   FC_TR(26);
 }
 template __global__ void k_fused_mag<false>(CompactArgs, SamplePlan, HdrInit, uint32_t);
@@ -1183,10 +1173,11 @@ template __global__ void k_fused_mag<true>(CompactArgs, SamplePlan, HdrInit, uin
 
 // --------------------------------------------------------------------------------------
 // k_resolve: exact T64 from the bracket's candidates (fast path, one launch).
-//   totals from the sharded counters -> rank r = k - #(key > t_hi) -> histogram bin beta
-//   holding rank r -> every workgroup gathers its chunks' candidates that fall in beta
-//   (candidate slot, or the entries slot when the chunk overflowed its candidate slot) ->
-//   the last workgroup sorts the <= 4096 survivors in LDS and picks T64.
+//   totals from the sharded counters -> rank r = k - #(key > t_hi) -> every workgroup bins its
+//   chunks' candidates (candidate slot, or the entries slot when the chunk overflowed its
+//   candidate slot) into the 4096-bin candidate histogram -> grid barrier -> the bin beta
+//   holding rank r -> every workgroup gathers its candidates in beta -> the last workgroup
+//   sorts the <= 4096 survivors in LDS and picks T64.
 // fc_topk_encode_dense (a.dense set, one client): k_compact_mag1_dense wrote q = g at every
 // LISTED element (comp >= L64); the slack ones (comp < T64) must go back to +0.  Every slack
 // entry is a candidate of its chunk, so the workgroups that gathered a chunk range wait for the
@@ -1208,6 +1199,8 @@ struct ResolveArgs {
   const fc_encode_job* jobs;   // batched encode (see CompactArgs)
   uint64_t ws_stride;
   float* dense;                // fc_topk_encode_dense: zero the slack of q (one client)
+  uint32_t rbin;               // 1: bin the candidates here (the compaction did not: batched,
+                               // unfused and rand-k); 0: k_fused_mag filled the histogram
 };
 
 constexpr int kResolveChunksMax = 2048;   // chunks per workgroup handled through LDS sizes
@@ -1223,39 +1216,39 @@ __global__ __launch_bounds__(kBlock) void k_resolve(ResolveArgs a0) {
   TopkState* S = a.W.st;
   const int tid = threadIdx.x;
   FC_TR(8);
-  const uint32_t gen0 = a.dense ? ld_agent(&S->gen) : 0u; // before the ticket: stable
-  // ---- totals (sharded counters written by k_compact), bracket and candidate histogram:
-  // one round of independent loads (they were three dependent rounds, ~9 us) ----
+  const uint32_t gen0 = a.dense ? ld_agent(&S->gen) : 0u; // before the tickets: stable
+  const uint32_t hgen0 = ld_agent(&S->hgen);
+  // ---- totals (sharded counters written by the compaction) and the bracket: one round of
+  // independent loads (they were three dependent rounds, ~9 us) ----
   uint32_t se = 0, sc = 0;
   if (tid < kShards) { se = S->shard_ent[tid]; sc = S->shard_cnd[tid]; }
   const uint32_t t_lo = S->t_lo, t_hi = S->t_hi, sbin = S->sbin, err = S->err;
+  const bool rbin = a.rbin != 0;
   uint32_t hv[kHistBins / kBlock];
 #pragma unroll
-  for (int j = 0; j < kHistBins / kBlock; ++j) hv[j] = a.W.chist[j * kBlock + tid];
+  for (int j = 0; j < kHistBins / kBlock; ++j) hv[j] = rbin ? 0u : a.W.chist[j * kBlock + tid];
   static_assert(kShards == 64, "shard totals: one wave");
   if (tid < 64) {
     se = wave_sum(se);
     sc = wave_sum(sc);
-    if (tid == 0) { s_tot[0] = se; s_tot[1] = sc; }
+    if (tid == 0) { s_tot[0] = se; s_tot[1] = sc; s_st = 0; }
   }
 #pragma unroll
-  for (int j = 0; j < kHistBins / kBlock; ++j) h[j * kBlock + tid] = hv[j];
+  for (int j = 0; j < kHistBins / kBlock; ++j) h[j * kBlock + tid] = hv[j];   // (rbin: zeros)
   __syncthreads();
   const uint32_t n_ent = s_tot[0], n_cand = s_tot[1];
   const uint32_t n_hi = n_ent - n_cand;                   // listed above the bracket
   const bool bad = err || n_cand > n_ent || (uint64_t)n_ent < a.k || (uint64_t)n_hi > a.k;
   const uint32_t rank = bad ? 0u : (uint32_t)(a.k - n_hi);
-  bool retry = bad;
+  const uint32_t per = (a.nchunks + gridDim.x - 1) / gridDim.x;
+  bool retry = bad || per > (uint32_t)kResolveChunksMax;  // grid-uniform (exact path)
   uint32_t beta = 0, r_in = 1, cnt_beta = 0;
-  if (!bad && rank > 0) {
+  if (!rbin && !retry && rank > 0) {                      // the compaction's histogram
     find_rank_desc(h, rank, s_tmp, s_out);
     beta = s_out[0]; r_in = s_out[1]; cnt_beta = h[beta];
     retry = cnt_beta > (uint32_t)kSmallCap || cnt_beta < r_in;
     __syncthreads();
   }
-  FC_TR(9);
-  const uint32_t per = (a.nchunks + gridDim.x - 1) / gridDim.x;
-  if (!bad && !retry && per > (uint32_t)kResolveChunksMax) retry = true;   // exact path
   // chunk range of this workgroup; gather sizes (candidate slot or, overflowed, entries)
   const uint32_t c0 = blockIdx.x * per;
   const uint32_t c1 = min(c0 + per, a.nchunks);
@@ -1277,7 +1270,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve(ResolveArgs a0) {
   constexpr int kGatherU = 8;
   uint32_t tpc = 64;
   while (tpc > 1 && tpc * nc > (uint32_t)kBlock) tpc >>= 1;
-  uint64_t v0[kGatherU];                                  // first pass, kept for the fix-up
+  uint64_t v0[kGatherU];                                  // first pass, kept for the later ones
 #pragma unroll
   for (int u = 0; u < kGatherU; ++u) v0[u] = ~0ull;
   // fn(v) for every pass of this thread over its candidates as comps (~0 = not a candidate:
@@ -1319,11 +1312,76 @@ __global__ __launch_bounds__(kBlock) void k_resolve(ResolveArgs a0) {
       }
     }
   };
-  if (walk && rank > 0) {
+  // ---- the candidate histogram: every workgroup bins the candidates of its chunk range in
+  // LDS and flushes the non-empty bins into one of kCandShards shards (one shared histogram
+  // queued ~94 same-address atomics per bin at 128 M); the last arriver (two-level ticket)
+  // sums the shards, finds the bin beta holding rank r and publishes it (generation word
+  // hgen).  (The compaction used to add every candidate into the histogram with a global
+  // atomic: 5.7 % of that pass at 128 M.)  The wait
+  // is safe: a client's <= 256 workgroups are dispatched together and never wait on a later
+  // client; the spin is bounded (sets err: the call reports RETRY). ----
+  const bool binning = rbin && !retry && rank > 0;       // grid-uniform
+  if (binning) {
+    for_cands(false, [&](const uint64_t (&v)[kGatherU]) {
+#pragma unroll
+      for (int u = 0; u < kGatherU; ++u)
+        if (v[u] != ~0ull) atomicAdd(&h[(((uint32_t)(v[u] >> a.ib)) - t_lo) >> sbin], 1u);
+    });
+    __syncthreads();
+    FC_TR(29);
+    {                                                     // this workgroup's shard
+      uint32_t* gh = a.W.chist + (blockIdx.x % kCandShards) * kHistBins;
+      for (int b = tid; b < kHistBins; b += kBlock)
+        if (h[b]) atomicAdd(&gh[b], h[b]);
+    }
+    FC_TR(27);
+    if (last_block_arrive_tree(a.W.tick + 2 * kTickWords, gridDim.x, blockIdx.x, &s_flag)) {
+      // the last arriver sums the shards (every load first, then the clearing stores: their
+      // next use is the next call's atomics, after this launch), finds beta and publishes it
+      constexpr int kPer = kHistBins / kBlock;
+      uint32_t t[kPer];
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) t[j] = 0;
+#pragma unroll
+      for (int sh = 0; sh < kCandShards; ++sh)
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) t[j] += ld_agent(&a.W.chist[sh * kHistBins + j * kBlock + tid]);
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) h[j * kBlock + tid] = t[j];
+      __syncthreads();
+      find_rank_desc(h, rank, s_tmp, s_out);
+      if (tid == 0) {
+        st_agent(&S->rb_beta, s_out[0]); st_agent(&S->rb_rin, s_out[1]);
+        st_agent(&S->rb_cnt, h[s_out[0]]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        st_agent(&S->hgen, hgen0 + 1u);
+      }
+      for (int i = tid; i < kHistBins * kCandShards / 4; i += kBlock)
+        reinterpret_cast<uint4*>(a.W.chist)[i] = make_uint4(0u, 0u, 0u, 0u);
+    } else if (tid == 0) {                                // relaxed sc1 poll (bounded)
+      uint32_t it = 0;
+      while (ld_agent(&S->hgen) == hgen0 && ++it < kSpinMax) __builtin_amdgcn_s_sleep(2);
+      if (it >= kSpinMax) { s_st = 1u; st_agent(&S->err, 1u); }
+    }
+    if (tid == 0 && s_st == 0) {
+      s_out[0] = ld_agent(&S->rb_beta); s_out[1] = ld_agent(&S->rb_rin); s_out[2] = ld_agent(&S->rb_cnt);
+    }
+    __syncthreads();
+    FC_TR(28);
+    if (s_st != 0) {
+      retry = true;                                       // (err makes the call RETRY)
+    } else {
+      beta = s_out[0]; r_in = s_out[1]; cnt_beta = s_out[2];
+      retry = cnt_beta > (uint32_t)kSmallCap || cnt_beta < r_in;
+    }
+    __syncthreads();
+  }
+  FC_TR(9);
+  if (!retry && rank > 0) {
     // gather bin beta into the LDS list (sv reused after the histogram)
     if (tid == 0) s_cnt = 0;
     __syncthreads();
-    for_cands(false, [&](const uint64_t (&v)[kGatherU]) {
+    for_cands(rbin, [&](const uint64_t (&v)[kGatherU]) {
 #pragma unroll
       for (int u = 0; u < kGatherU; ++u) {
         if (v[u] != ~0ull && ((((uint32_t)(v[u] >> a.ib)) - t_lo) >> sbin) == beta) {
@@ -1400,10 +1458,13 @@ __global__ __launch_bounds__(kBlock) void k_resolve(ResolveArgs a0) {
   FC_TR(12);
   // ---- last workgroup ----
   const uint64_t T = select_T();
-  const uint32_t status = retry ? (uint32_t)FC_STATUS_RETRY_EXACT : (uint32_t)FC_STATUS_OK;
+  // another workgroup's timed-out wait for the bins (sticky err) also makes the call retry
+  const bool other_err = ld_agent(&S->err) != 0u;
+  const uint32_t status = retry || other_err ? (uint32_t)FC_STATUS_RETRY_EXACT : (uint32_t)FC_STATUS_OK;
   FC_TR(14);
-  if (a.dense && walk && !retry) fixup(T);
-  for (int b = tid; b < kHistBins; b += kBlock) a.W.chist[b] = 0;   // for the next call
+  if (a.dense && walk && !retry && !other_err) fixup(T);
+  if (!rbin)                                            // the compaction's bins, for the next call
+    for (int b = tid; b < kHistBins; b += kBlock) a.W.chist[b] = 0;
   if (tid == 0) {
     a.hdr->thresh = T;
     a.hdr->n_entries = n_ent;

@@ -46,7 +46,7 @@ def main():
     # "fused": k_fused_mag's chunk workgroups (24 loads issued, 25 bracket received, 26 done),
     # on the sample's clock (same launch)
     for name, slots in (("sample", [0, 20, 21, 22, 2, 3, 4, 18, 19, 5, 7, 23, 6]), ("fused", [24, 25, 26]),
-                        ("resolve", [8, 9, 10, 11, 16, 17, 12, 13, 14, 15])):
+                        ("resolve", [8, 10, 29, 27, 28, 9, 11, 16, 17, 12, 14, 13, 15])):
         rec = t[:, slots[0]] > 0
         if name != "fused":
             t0 = t[rec, slots[0]].min() if rec.any() else 0.0
