@@ -55,6 +55,9 @@ def parse():
                     help="nccl (RCCL over xGMI: the measurement) or gloo (rehearsal only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-single", action="store_true", help="skip the single-gradient probe")
+    ap.add_argument("--pipeline", action="store_true",
+                    help="fold each encode chain's packets on its stream as soon as they are "
+                         "encoded (codec.encode_fold_batch; measured no faster, A/B only)")
     ap.add_argument("--no-batch", action="store_true",
                     help="encode client by client (fc_topk_encode) instead of batched")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r02_pmc_k_compact_mag1.json"),
@@ -252,23 +255,37 @@ def main():
     status_host = torch.empty((M, 4), dtype=torch.uint8, pin_memory=True)
     encoded = torch.cuda.Event()
 
+    pipelined = args.pipeline and not args.no_batch
+    w_local = [float(x) for x in w_all[rows.start:rows.stop]]
+    folded = lambda rows_, w_, out_, cont_: None    # noqa: E731 (the fold already ran)
+
     def step():
-        if args.no_batch:
-            for i in range(M):
-                codec.encode_top(grads[i], k, packet=pkts[i], check=False)
-        else:                                       # 4 launches for all M clients
-            codec.encode_top_batch(grads, k, packets=pkts, jobs=jobs, check=False,
-                                   streams=args.streams)
-        # local fold of this rank's shard (k_fold_q) + RCCL fp32 reduce to rank 0, launched
-        # before the host reads the statuses (no host round trip between encode and fold)
-        status_host.copy_(hdrs[:, 36:40], non_blocking=True)   # fc_packet_hdr.status
-        encoded.record()
         b = nstep[0] & 1
         nstep[0] += 1
         if works[b] is not None:
             works[b].wait()                         # stream-side wait for step i-2's reduce
-        works[b] = fedavg.aggregate(fold, M * world, accs[b], weights=w_all, async_op=True)
-        encoded.synchronize()
+        if pipelined:
+            # each encode chain's packets are folded (k_fold_q) on its stream as soon as they
+            # are encoded, the second fold continuing the first's partial sum in row order;
+            # the statuses are copied once every chain is encoded (`ready`)
+            ready = codec.encode_fold_batch(grads, k, w_local, accs[b], packets=pkts, jobs=jobs,
+                                            views=views, streams=args.streams,
+                                            status=(hdrs[:, 36:40], status_host))
+        else:
+            if args.no_batch:
+                for i in range(M):
+                    codec.encode_top(grads[i], k, packet=pkts[i], check=False)
+            else:                                   # 4 launches for all M clients
+                codec.encode_top_batch(grads, k, packets=pkts, jobs=jobs, check=False,
+                                       streams=args.streams)
+            status_host.copy_(hdrs[:, 36:40], non_blocking=True)   # fc_packet_hdr.status
+            encoded.record()
+            ready = encoded
+        # this rank's fold (unless pipelined above) + RCCL fp32 reduce to rank 0, queued before
+        # the host waits for the statuses (it queues the next step while the fold runs)
+        works[b] = fedavg.aggregate(folded if pipelined else fold, M * world, accs[b],
+                                    weights=w_all, async_op=True)
+        ready.synchronize()
         if bool((status_host != 0).any()):          # sampled bracket missed: exact re-encode
             redo_total[0] += codec.resolve(pkts)    # and fold again (after the first reduce)
             if works[b] is not None:

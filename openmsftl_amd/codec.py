@@ -349,6 +349,80 @@ def encode_top_batch(grads: Sequence[torch.Tensor], k: int, *,
     return list(packets)
 
 
+def encode_fold_batch(grads: Sequence[torch.Tensor], k: int, weights, out: torch.Tensor, *,
+                      packets: Sequence[Packet], jobs: Optional[torch.Tensor] = None,
+                      views: Optional[torch.Tensor] = None, streams: int = 2,
+                      status: Optional[tuple] = None) -> "torch.cuda.Event":
+    """Batched top-k encode of M gradients AND their packet FedAVG fold (gar.py:44), pipelined:
+    sub-batch i is encoded on forked stream i and folded there as soon as it is encoded,
+    continuing sub-batch i-1's partial sum (an event orders the folds, so the rows are added
+    in G's order: bit-identical to :func:`encode_top_batch` + :func:`decode_accumulate`), while
+    sub-batch i+1 still encodes on its own stream.  ``out`` holds the aggregate once the
+    caller's stream (joined at return) reaches it.  Returns an event recorded once every
+    sub-batch is ENCODED (the folds may still run); ``status=(src, dst)``: ``dst.copy_(src)``
+    (e.g. the packet headers' status words into pinned host memory) is queued right then, so
+    the host can check the statuses while the last fold runs.  No re-encode here: call
+    :func:`resolve` and, if it re-encoded anything, fold again (bench.py does)."""
+    lib = L.load()
+    m = len(grads)
+    if m == 0 or len(packets) != m:
+        raise ValueError("one packet per gradient, at least one")
+    n, dev = grads[0].numel(), grads[0].device
+    if not 0 < k < n:
+        raise ValueError("encode_fold_batch needs 0 < k < n")
+    weights = [float(x) for x in weights]
+    if len(weights) != m:
+        raise ValueError("one weight per gradient")
+    if jobs is None:
+        jobs = encode_jobs(grads, packets)
+    if views is None:
+        views = views_tensor(packets, weights, dev)
+    nside = max(1, min(int(streams), m, _MAX_SIDE))
+    groups = [(i + 1) * m // nside - i * m // nside for i in range(nside)]
+    jb, vb = ctypes.sizeof(L.EncodeJob), ctypes.sizeof(L.PacketView)
+    main = torch.cuda.current_stream(dev)
+    sides = _side_streams(dev, nside)
+    start = torch.cuda.Event()
+    start.record(main)
+    prev = None
+    encoded = []
+    lo = 0
+    for i, size in enumerate(groups):
+        hi = lo + size
+        side = sides[i]
+        with torch.cuda.stream(side):
+            side.wait_event(start)
+            ws = BatchWorkspace.get(n, size, dev)
+            L.check(lib.fc_topk_encode_batch(ctypes.c_void_p(jobs.data_ptr() + lo * jb), size, n, k,
+                                             L.FC_KEY_MAGNITUDE, packets[0].capacity, _vp(ws.buf),
+                                             ws.nbytes, _stream(dev)), "fc_topk_encode_batch")
+            for p, g in zip(packets[lo:hi], grads[lo:hi]):
+                p.k = k
+                p._enc = (g, k, L.FC_KEY_MAGNITUDE, 0, 0)
+            ev = torch.cuda.Event()
+            ev.record(side)
+            encoded.append(ev)
+            if i == len(groups) - 1:                       # every sub-batch is encoded here
+                for e in encoded[:-1]:
+                    side.wait_event(e)
+                if status is not None:
+                    status[1].copy_(status[0], non_blocking=True)
+                done = torch.cuda.Event()
+                done.record(side)
+            if prev is not None:
+                side.wait_event(prev)                      # folds in G's row order
+            fn = lib.fc_decode_accumulate_continue if i else lib.fc_decode_accumulate
+            L.check(fn(ctypes.c_void_p(views.data_ptr() + lo * vb), size, L.FC_FMT_IDXVAL, n,
+                       _vp(out), _stream(dev)), "fc_decode_accumulate")
+            prev = torch.cuda.Event()
+            prev.record(side)
+        lo = hi
+    main.wait_event(prev)
+    for side in sides:                                     # later frees stay ordered
+        main.wait_stream(side)
+    return done
+
+
 def resolve(packets: Sequence[Packet]) -> int:
     """Re-encode (exact path) every top/rand packet whose sampled bracket missed.
     Returns the number of packets that needed the exact path."""

@@ -80,18 +80,20 @@ __device__ void find_ranks_desc(const uint32_t* h, uint32_t r1, uint32_t r2, uin
   const int t = threadIdx.x;
   constexpr int per = kHistBins / kBlock;
   const int top = kHistBins - 1 - per * t;
-  uint32_t hv[per], sum = 0;
+  uint32_t sum = 0;
 #pragma unroll
-  for (int b = 0; b < per; ++b) { hv[b] = h[top - b]; sum += hv[b]; }
+  for (int b = 0; b < per; ++b) sum += h[top - b];
   uint32_t total;
   const uint32_t excl = block_excl_scan(sum, s_tmp, &total);
+  // the bins are re-read from LDS (only the one thread whose range holds r walks them): 16
+  // live histogram registers pushed k_fused_mag's sample part into scratch
   auto find = [&](uint32_t r, int o) {
     if (r > excl && r <= excl + sum) {
       uint32_t c = excl;
-#pragma unroll
       for (int b = 0; b < per; ++b) {
-        if (r > c && r <= c + hv[b]) { s_out[o] = (uint32_t)(top - b); s_out[o + 1] = r - c; }
-        c += hv[b];
+        const uint32_t hb = h[top - b];
+        if (r <= c + hb) { s_out[o] = (uint32_t)(top - b); s_out[o + 1] = r - c; break; }
+        c += hb;
       }
     }
     if (t == 0 && !(r >= 1 && r <= total)) { s_out[o] = 0; s_out[o + 1] = 1; }
@@ -176,7 +178,7 @@ __device__ __forceinline__ void seg_lane(const SamplePlan& P, uint32_t s, int ti
 
 // Pilot level-1 histogram (key >> 19) of the kPilotSegs pilot segments -> the window.
 // own: this workgroup IS workgroup 0 (its segments xs / es / ls are the pilot, already loaded).
-template <int KM>
+template <int KM, bool OWN_ONLY = false>
 __device__ __forceinline__ FineWin pilot_window(const float* __restrict__ g, const SamplePlan& P,
                                                 uint64_t seed, uint64_t off, uint32_t* h,
                                                 uint32_t* s_tmp, uint32_t* s_out, bool own,
@@ -189,7 +191,7 @@ __device__ __forceinline__ FineWin pilot_window(const float* __restrict__ g, con
   uint32_t ep[kPilotSegs], lp[kPilotSegs];
 #pragma unroll
   for (int q = 0; q < kPilotSegs; ++q) {
-    if (own) {
+    if (OWN_ONLY || own) {
       xp[q] = xs[q]; ep[q] = es[q]; lp[q] = ls[q];
       continue;
     }
@@ -236,7 +238,9 @@ struct SampleShared {
 // The body of k_sample1 for workgroup bid of nb (256 threads).  shared_pilot: a lone client's
 // launch (workgroup 0 publishes the window).  pub != 0 (k_fused_mag): once the bracket is
 // written, publish it to the compaction workgroups of the same launch (S->fz_pub = pub).
-template <int KM>
+// SHARED_ONLY: the launch is a lone client's (the window always comes from workgroup 0's own
+// segments): no second set of pilot registers (k_fused_mag runs in 64 VGPRs)
+template <int KM, bool SHARED_ONLY = false>
 __device__ __forceinline__ void sample_body(const float* __restrict__ g, const SamplePlan& P,
                                             uint64_t seed, uint64_t off, const WsPtrs& W,
                                             uint32_t ib, fc_packet_hdr* hdr, const HdrInit& HI,
@@ -264,8 +268,9 @@ __device__ __forceinline__ void sample_body(const float* __restrict__ g, const S
   }
   for (int b = tid; b < kHistBins; b += kBlock) h[b] = 0;
   FineWin F;
+  if (SHARED_ONLY) shared_pilot = true;
   if (!shared_pilot || bid == 0) {
-    F = pilot_window<KM>(g, P, seed, off, h, s_tmp, s_out, bid == 0, xs, es, ls);
+    F = pilot_window<KM, SHARED_ONLY>(g, P, seed, off, h, s_tmp, s_out, bid == 0, xs, es, ls);
     if (shared_pilot && tid == 0) {               // publish: sc1 payload, drained, sc1 flag
       st_agent(&S->win_klo, F.klo); st_agent(&S->win_khi, F.khi); st_agent(&S->win_fs, F.fs);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1131,6 +1136,9 @@ __global__ __launch_bounds__(kCBlock, FC_MAG1_WAVES_PER_EU) void k_compact_mag1_
 // never waits on a chunk workgroup, so no wait can deadlock; a timed-out one (never expected)
 // sets S->err, and the resolve reports RETRY (the caller re-encodes exactly).
 // --------------------------------------------------------------------------------------
+#ifndef FC_FZ_SLEEP
+#define FC_FZ_SLEEP 4         // s_sleep argument of the chunk workgroups' bracket poll
+#endif
 union FusedShared {
   SampleShared s;
   MagShared m;
@@ -1145,7 +1153,7 @@ __global__ __launch_bounds__(kCBlock, FC_MAG1_WAVES_PER_EU) void k_fused_mag(Com
   const uint32_t pub = sload2(&S->fz_seq).x + 1u;   // not written by this launch
   if (blockIdx.x < nsamp) {
     if (threadIdx.x >= kBlock) return;
-    sample_body<kKeyMag>(a0.g, P, 0ull, 0ull, a0.W, a0.ib, a0.hdr, HI, blockIdx.x, nsamp, true, u.s, pub);
+    sample_body<kKeyMag, true>(a0.g, P, 0ull, 0ull, a0.W, a0.ib, a0.hdr, HI, blockIdx.x, nsamp, true, u.s, pub);
     return;
   }
   const uint32_t chunk = blockIdx.x - nsamp;
@@ -1154,7 +1162,7 @@ __global__ __launch_bounds__(kCBlock, FC_MAG1_WAVES_PER_EU) void k_fused_mag(Com
   FC_TR(24);
   if (threadIdx.x == 0) {
     uint32_t it = 0;
-    while (ld_agent(&S->fz_pub) != pub && ++it < kSpinMax) __builtin_amdgcn_s_sleep(4);
+    while (ld_agent(&S->fz_pub) != pub && ++it < kSpinMax) __builtin_amdgcn_s_sleep(FC_FZ_SLEEP);
     if (it >= kSpinMax) st_agent(&S->err, 1u);
     MagState m;
     m.L64 = ld_agent(&S->L64);

@@ -347,6 +347,34 @@ def test_batch_encode_forked_streams(streams, groups):
         _check_top_packet(x, k, pb, codec.decode(pb).cpu().numpy())
 
 
+@pytest.mark.parametrize("M,streams", [(5, 2), (7, 3), (2, 2), (1, 2)])
+def test_encode_fold_batch_pipelined(M, streams):
+    """encode_fold_batch (each sub-batch folded on its stream as soon as it is encoded, the
+    folds chained in row order) gives the packets of encode_top_batch and, bit for bit, the
+    FedAVG of gar.py:44 on the G those packets decode to (oracle)."""
+    codec = _codec()
+    n, f = 300_001, 0.1
+    rng = np.random.default_rng(91 + M)
+    host = [(rng.standard_normal(n) * 10.0 ** rng.uniform(-4, 1)).astype(np.float32)
+            for _ in range(M)]
+    grads = [torch.from_numpy(x).cuda() for x in host]
+    k = co.effective_k(co.num_kept(f, n), n)
+    w = np.full(M, 1.0 / M, dtype=np.float32)            # gar.py:37-40's default weights
+    pk = [codec.Packet.alloc(n, codec.L.FC_FMT_IDXVAL, grads[0].device, k=k) for _ in range(M)]
+    out = torch.empty(n, dtype=torch.float32, device="cuda")
+    for _ in range(2):                                   # reused buffers, second pass too
+        codec.encode_fold_batch(grads, k, w, out, packets=pk, streams=streams)
+        assert codec.resolve(pk) == 0
+        torch.cuda.synchronize()
+    ref = codec.encode_top_batch(grads, k)
+    for a, b in zip(pk, ref):
+        assert _packet_bytes(a) == _packet_bytes(b)
+    G = go.build_dense_G([co.compress({"compression_function": "top", "fraction_coordinate": f}, x)
+                          for x in host], np.float32)
+    want = go.FedAvgOracle({}).aggregate(G)
+    assert out.cpu().numpy().tobytes() == want.tobytes()
+
+
 def test_batch_encode_philox_and_fallback():
     """Native rand-k keys per client (seed/offset per job) and one client whose sampled
     bracket misses (resolved by the per-packet exact path) inside the same batch."""

@@ -1,8 +1,24 @@
+# One A/B box pass: GPU parity tests, single-gradient variants (VARS), then the bench with and
+# without the pipelined encode+fold (configs[2] and the headline step).
 set -e
-bash tools/gpu_ab.sh dual
-N=16777216 B=64 VARS="rgb32 rgb64" bash tools/ab_batch16.sh
-N=134217728 B=16 IT=6 VARS="rgb32 rgb64" bash tools/ab_batch16.sh
-timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/dual_bench.json 2> gpurun_out/dual_bench.err
+OUT=gpurun_out/${TAG:-ab}
+mkdir -p $OUT
+if [ -z "$SKIP_TESTS" ]; then
+timeout -k 10 400 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread \
+  > $OUT/gpu_tests.log 2>&1 || { tail -40 $OUT/gpu_tests.log; exit 1; }
+tail -1 $OUT/gpu_tests.log
+fi
+[ -n "$VARS" ] && bash tools/ab_single.sh
+summ() {
 python3 -c "
-import json; d=json.load(open('gpurun_out/dual_bench.json')); e=d['extra']
-print(json.dumps({'value':d['value'],'ms':d['ms_per_step'],'roof':d['roofline']['frac'],'k':{c:v['avg_us'] for c,v in e['per_step_kernel_time'].items() if c!='note'},'single':e['single_gradient']['fused_dense'],'c1':e['configs_1_2']['config1_single_16M']['fused_dense'],'c2':e['configs_1_2']['config2_128x16M']['hbm_frac'], 'c2ms':e['configs_1_2']['config2_128x16M']['ms_per_step'],'self':e['self_check'][:3]}))"
+import json,sys; d=json.load(open(sys.argv[1])); e=d['extra']
+print(json.dumps({'tag':sys.argv[2],'value':d['value'],'ms':d['ms_per_step'],'roof':d['roofline']['frac'],'k':{c:v['avg_us'] for c,v in e['per_step_kernel_time'].items() if c!='note'},'single':e.get('single_gradient',{}).get('fused_dense'),'c1':e.get('configs_1_2',{}).get('config1_single_16M',{}).get('fused_dense'),'c2':e.get('configs_1_2',{}).get('config2_128x16M',{}).get('hbm_frac'),'c2ms':e.get('configs_1_2',{}).get('config2_128x16M',{}).get('ms_per_step'),'self':e['self_check'][:3]}))" $1 $2
+}
+for B in $BENCH; do
+  case $B in
+    pipe) A="" ;;
+    nopipe) A="--no-pipeline" ;;
+  esac
+  timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 150 $A > $OUT/bench_$B.json 2> $OUT/bench_$B.err
+  summ $OUT/bench_$B.json $B
+done
