@@ -1003,8 +1003,15 @@ __device__ __forceinline__ MagState mag_state(const TopkState* S) {
   return m;
 }
 
-// The chunk's 16 elements per lane in the ballot layout: whole chunk = nt loads; the last,
-// partial chunk clamps its addresses (its values past n are never listed: exact path).
+// The chunk's 16 elements per lane in the ballot layout; the last, partial chunk clamps its
+// addresses (its values past n are never listed: exact path).  Non-temporal loads: plain ones
+// stream this shape faster in isolation (5.77-5.84 against 5.53-5.55 TB/s,
+// tools/shape_probe.hip) but are equal in the batched compaction and 15 % slower on the dense
+// path, whose 512 MB of q stores then compete with the gradient for the caches
+// (profiles/r02_ab_mag_load_kind.jsonl).
+#ifndef FC_MAG_NT_LOAD
+#define FC_MAG_NT_LOAD 1
+#endif
 template <int NW>
 __device__ __forceinline__ void mag_load(const float* g, uint32_t chunk, uint64_t n,
                                          float (&x)[MagGeo<NW>::kQ]) {
@@ -1021,7 +1028,13 @@ __device__ __forceinline__ void mag_load(const float* g, uint32_t chunk, uint64_
   }
   gf* gp = (gf*)g + base + l0;
 #pragma unroll
-  for (int q = 0; q < NQ; ++q) x[q] = __builtin_nontemporal_load(gp + (q >> 2) * IS + (q & 3) * 64);
+  for (int q = 0; q < NQ; ++q) {
+#if FC_MAG_NT_LOAD
+    x[q] = __builtin_nontemporal_load(gp + (q >> 2) * IS + (q & 3) * 64);
+#else
+    x[q] = gp[(q >> 2) * IS + (q & 3) * 64];
+#endif
+  }
 }
 
 // One workgroup per item (grid = (nchunks, clients)); <= 64 VGPRs, so 4 resident 512-thread
