@@ -1245,6 +1245,13 @@ __global__ __launch_bounds__(kBlock) void k_resolve(ResolveArgs a0) {
   if (tid < kShards) { se = S->shard_ent[tid]; sc = S->shard_cnd[tid]; }
   const uint32_t t_lo = S->t_lo, t_hi = S->t_hi, sbin = S->sbin, err = S->err;
   const bool rbin = a.rbin != 0;
+  // this workgroup's chunk range and (<= one per thread, the usual case) its candidate counts,
+  // in the same round of loads
+  const uint32_t per = (a.nchunks + gridDim.x - 1) / gridDim.x;
+  const uint32_t c0 = blockIdx.x * per;
+  const uint32_t c1 = min(c0 + per, a.nchunks);
+  const uint32_t nc = c1 > c0 ? c1 - c0 : 0u;
+  const uint32_t cc_early = (nc <= (uint32_t)kBlock && (uint32_t)tid < nc) ? a.W.ccnt[c0 + tid] : 0u;
   uint32_t hv[kHistBins / kBlock];
 #pragma unroll
   for (int j = 0; j < kHistBins / kBlock; ++j) hv[j] = rbin ? 0u : a.W.chist[j * kBlock + tid];
@@ -1261,7 +1268,6 @@ __global__ __launch_bounds__(kBlock) void k_resolve(ResolveArgs a0) {
   const uint32_t n_hi = n_ent - n_cand;                   // listed above the bracket
   const bool bad = err || n_cand > n_ent || (uint64_t)n_ent < a.k || (uint64_t)n_hi > a.k;
   const uint32_t rank = bad ? 0u : (uint32_t)(a.k - n_hi);
-  const uint32_t per = (a.nchunks + gridDim.x - 1) / gridDim.x;
   bool retry = bad || per > (uint32_t)kResolveChunksMax;  // grid-uniform (exact path)
   uint32_t beta = 0, r_in = 1, cnt_beta = 0;
   if (!rbin && !retry && rank > 0) {                      // the compaction's histogram
@@ -1270,17 +1276,13 @@ __global__ __launch_bounds__(kBlock) void k_resolve(ResolveArgs a0) {
     retry = cnt_beta > (uint32_t)kSmallCap || cnt_beta < r_in;
     __syncthreads();
   }
-  // chunk range of this workgroup; gather sizes (candidate slot or, overflowed, entries)
-  const uint32_t c0 = blockIdx.x * per;
-  const uint32_t c1 = min(c0 + per, a.nchunks);
-  const uint32_t nc = c1 > c0 ? c1 - c0 : 0u;
   const bool walk = !retry && (rank > 0 || a.dense);      // uniform
   // ---- per-chunk gather sizes: the candidate slot, or (bit 31) the entries slot of a chunk
   // whose candidates overflowed their slot ----
   if (walk) {
     for (uint32_t lc = tid; lc < nc; lc += kBlock) {
       const uint32_t c = c0 + lc;
-      const uint32_t cc = a.W.ccnt[c];
+      const uint32_t cc = nc <= (uint32_t)kBlock ? cc_early : a.W.ccnt[c];
       s_pre[lc] = cc > (uint32_t)kCandSlot ? (a.cnt[c] | 0x80000000u) : cc;
     }
     __syncthreads();
@@ -1419,15 +1421,27 @@ __global__ __launch_bounds__(kBlock) void k_resolve(ResolveArgs a0) {
       if (s_base + q < (uint32_t)kSmallCap) st_agent(&a.W.small[s_base + q], sv[q]);
   }
   FC_TR(11);
-  // dense fix-up of this workgroup's range once T64 is known: q[idx] = +0 for comp < T64
-  auto fixup = [&](uint64_t T) {
-    const uint64_t imask = (1ull << a.ib) - 1;
-    for_cands(rank > 0, [&](const uint64_t (&v)[kGatherU]) {
+  // dense fix-up of this workgroup's range: q[idx] = +0 for every listed comp < T64.  Bins are
+  // in key order, so a candidate binned below beta is below T64 whatever T64 is: those are
+  // zeroed right after the gather ticket (zero_below, while T64 is being picked); once T64 is
+  // known only bin beta is left (fixup).  rank == 0: every candidate is slack (fixup alone).
+  const uint64_t imask = (1ull << a.ib) - 1;
+  auto bin_of = [&](uint64_t v) { return (((uint32_t)(v >> a.ib)) - t_lo) >> sbin; };
+  auto zero_below = [&]() {
+    for_cands(true, [&](const uint64_t (&v)[kGatherU]) {
 #pragma unroll
       for (int u = 0; u < kGatherU; ++u)
-        if (v[u] < T) a.dense[v[u] & imask] = 0.0f;       // ~0 (not a candidate) is never < T
+        if (v[u] != ~0ull && bin_of(v[u]) < beta) a.dense[v[u] & imask] = 0.0f;
     });
   };
+  auto fixup = [&](uint64_t T, bool only_beta) {
+    for_cands(rank > 0, [&](const uint64_t (&v)[kGatherU]) {
+#pragma unroll
+      for (int u = 0; u < kGatherU; ++u)                  // ~0 (not a candidate) is never < T
+        if (v[u] < T && (!only_beta || bin_of(v[u]) == beta)) a.dense[v[u] & imask] = 0.0f;
+    });
+  };
+  const bool split_fix = a.dense && walk && !retry && rank > 0;   // (after the gather: v0 set)
   // T64 from the gathered list: thread i ranks candidate i by counting the larger ones (comps
   // are unique; <= 256 candidates) or, for a larger bin, an LDS bitonic sort
   auto select_T = [&]() -> uint64_t {
@@ -1461,6 +1475,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve(ResolveArgs a0) {
     if (tid == 0 && a.dense) st_agent(&S->gen, gen0 + 1u);
   } else {
     if (!a.dense || !walk) return;
+    if (split_fix) zero_below();                        // while T64 is being picked
     if (tid == 0) {                                     // relaxed sc1 poll (bounded)
       uint32_t it = 0;
       while (ld_agent(&S->gen) == gen0 && ++it < kSpinMax) __builtin_amdgcn_s_sleep(4);
@@ -1472,18 +1487,18 @@ __global__ __launch_bounds__(kBlock) void k_resolve(ResolveArgs a0) {
     if (s_st != 0) return;
     const uint64_t T = select_T();
     FC_TR(14);
-    if (!retry) fixup(T);
+    if (!retry) fixup(T, split_fix);
     FC_TR(13);
     return;
   }
   FC_TR(12);
-  // ---- last workgroup ----
+  // ---- last workgroup (nothing left to overlap: T64 first, then one full fix-up pass) ----
   const uint64_t T = select_T();
   // another workgroup's timed-out wait for the bins (sticky err) also makes the call retry
   const bool other_err = ld_agent(&S->err) != 0u;
   const uint32_t status = retry || other_err ? (uint32_t)FC_STATUS_RETRY_EXACT : (uint32_t)FC_STATUS_OK;
   FC_TR(14);
-  if (a.dense && walk && !retry && !other_err) fixup(T);
+  if (a.dense && walk && !retry && !other_err) fixup(T, false);
   if (!rbin)                                            // the compaction's bins, for the next call
     for (int b = tid; b < kHistBins; b += kBlock) a.W.chist[b] = 0;
   if (tid == 0) {
