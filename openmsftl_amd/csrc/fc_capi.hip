@@ -77,7 +77,19 @@ static uint32_t decode_grid(uint64_t n, uint32_t per_cu = kDecBlocksPerCU) {
 #ifndef FC_SAMPLE_DIV
 #define FC_SAMPLE_DIV 64                          // sample 1/64 of the gradient (below the cap)
 #endif
-static SamplePlan make_plan(uint64_t n, uint64_t k) {
+// fc_topk_encode_dense (the drop-in compress('top') path) samples more: its sample latency
+// hides under the fused launch's first round of chunk loads, and a narrower bracket means
+// fewer candidates on its critical path (16 M: 256 -> 512 segments took 68.8 -> 60.8 us; the
+// 128-client bench step got slower with a bigger sample: profiles/r02_ab_sample_plan.jsonl).
+// Its dense result does not depend on the bracket; packet encodes keep the batched plan, so a
+// single encode_top and a batched one write the same packet bytes (slack included).
+#ifndef FC_SAMPLE_DIV_SINGLE
+#define FC_SAMPLE_DIV_SINGLE 32
+#endif
+#ifndef FC_MAX_SAMPLE_SEGS_SINGLE
+#define FC_MAX_SAMPLE_SEGS_SINGLE 2048
+#endif
+static SamplePlan make_plan(uint64_t n, uint64_t k, bool single = false) {
   SamplePlan P;
   memset(&P, 0, sizeof P);
   P.n = n;
@@ -88,9 +100,10 @@ static SamplePlan make_plan(uint64_t n, uint64_t k) {
   } else {
     // 1/64 of the gradient, 64..1024 segments: at 16 M a 64-client batch spends 1391 us in
     // sample + compact + resolve with 256 segments against 1481 us with 512 (1/32)
-    uint64_t seg = n / FC_SAMPLE_DIV / 1024;
+    uint64_t seg = n / (single ? FC_SAMPLE_DIV_SINGLE : FC_SAMPLE_DIV) / 1024;
     if (seg < 64) seg = 64;
-    if (seg > FC_MAX_SAMPLE_SEGS) seg = FC_MAX_SAMPLE_SEGS;
+    const uint64_t cap = single ? FC_MAX_SAMPLE_SEGS_SINGLE : FC_MAX_SAMPLE_SEGS;
+    if (seg > cap) seg = cap;
     P.nseg = (uint32_t)seg;
     const double S = (double)seg * 1024.0;
     const double q = (double)k / (double)n;
@@ -366,7 +379,7 @@ int fc_topk_encode_dense(const float* g, uint64_t n, uint64_t k, uint16_t* idx, 
   if (rc) return rc;
   ca.dense = dense;
   hipStream_t s = (hipStream_t)stream;
-  const SamplePlan P = make_plan(n, k);
+  const SamplePlan P = make_plan(n, k, true);
   const uint32_t sgrid = (P.nseg + kSampleSegs - 1) / kSampleSegs;
   if (fused_enabled()) {
     rc = launch_fused(ca, P, hi, sgrid, s);
