@@ -347,14 +347,15 @@ __device__ __forceinline__ void sample_body(const float* __restrict__ g, const S
     S->n_cand = 0; S->cand_over = 0; S->ent_over = 0;
     S->win_flag = 0;               // (err: set by a timed-out wait, read and
                                                   // cleared by this call's k_resolve)
-    // the header's only writer in this launch: a static header written by workgroup 0 at its
-    // start raced this store through another XCD's L2 (lower read back as 0)
-    write_hdr_static(hdr, HI);
-    hdr->lower = (uint64_t)t_lo << ib;
-    if (pub) {
+    if (pub) {                     // the compaction's state first: the header waits
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       st_agent(&S->fz_pub, pub);
     }
+    // the header's only writer in this launch: a static header written by workgroup 0 at its
+    // start raced this store through another XCD's L2 (lower read back as 0).  Nothing in this
+    // launch reads it (k_resolve does, after the kernel boundary).
+    write_hdr_static(hdr, HI);
+    hdr->lower = (uint64_t)t_lo << ib;
   }
   // clear the shards for the next call last, with plain 16-B stores (their next use is an
   // atomic in the next launch, after this kernel's end-of-launch write-back)
