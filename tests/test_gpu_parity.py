@@ -161,6 +161,50 @@ def test_top_bracket_miss_falls_back_to_exact():
     _check_top_packet(g, k, pkt, out)
 
 
+def _wave_overflow_gradient(n=4 << 20, f=0.1, seed=5):
+    """A gradient whose chunk 7 holds ~100 candidates (|g| within 1e-5 of the k-th
+    magnitude) in wave 3's elements alone -- past that wave's 32-entry candidate sub-slot
+    while the chunk stays under its 256-entry candidate slot -- and chunk 9 holds 40 spread
+    over two waves (no overflow)."""
+    rng = np.random.default_rng(seed)
+    g = rng.standard_normal(n, dtype=np.float32)
+    k = co.effective_k(co.num_kept(f, n), n)
+    T = np.partition(np.abs(g), n - k)[n - k]
+    def near(m):
+        v = T * (1.0 + rng.uniform(-1e-5, 1e-5, m))
+        return (v * rng.choice([-1.0, 1.0], m)).astype(np.float32)
+    lay = lambda base, w: (base + np.arange(4)[:, None, None] * 2048 + w * 256
+                           + np.arange(4)[None, :, None] * 64 + np.arange(64)[None, None, :]).ravel()
+    pos = rng.choice(lay(7 * 8192, 3), 100, replace=False)
+    g[pos] = near(100)
+    pos = np.concatenate([rng.choice(lay(9 * 8192, 1), 20, replace=False),
+                          rng.choice(lay(9 * 8192, 6), 20, replace=False)])
+    g[pos] = near(40)
+    return g, k
+
+
+@pytest.mark.parametrize("path", ["single", "batch", "dense"])
+def test_top_wave_candidate_overflow(path):
+    """Per-wave candidate sub-slots (k_compact_mag1 / k_fused_mag): a wave with more than 32
+    candidates marks its chunk overflowed and the resolve re-reads the chunk's entries; the
+    result is still the oracle's, on the fused single-client path (compaction-side bins), the
+    batched path (resolve-side bins) and the dense path."""
+    g, k = _wave_overflow_gradient()
+    codec = _codec()
+    if path == "single":
+        pkt, out = _gpu_topk(g, k)
+        _check_top_packet(g, k, pkt, out)
+    elif path == "batch":
+        g2 = _wave_overflow_gradient(seed=6)[0]
+        grads = [torch.from_numpy(x).cuda() for x in (g, g2)]
+        pk = codec.encode_top_batch(grads, k)
+        for x, p in zip((g, g2), pk):
+            _check_top_packet(x, k, p, codec.decode(p).cpu().numpy())
+    else:
+        pkt, q = _dense_top(g, k)
+        _check_top_packet(g, k, pkt, q)
+
+
 # ---- top straight to the dense q (fc_topk_encode_dense: compaction streams q + fix-up) ----
 def _dense_top(g_np, k):
     codec = _codec()
