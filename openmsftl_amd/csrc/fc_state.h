@@ -35,8 +35,14 @@ struct alignas(16) TopkState {
 };
 static_assert(sizeof(TopkState) <= 1024, "state block");
 
-constexpr int kSampleShards = 8;            // k_sample1's global histogram, sharded by workgroup
-constexpr int kCandShards = 8;              // k_resolve's candidate histogram, likewise
+#ifndef FC_SAMPLE_SHARDS
+#define FC_SAMPLE_SHARDS 8
+#endif
+#ifndef FC_CAND_SHARDS
+#define FC_CAND_SHARDS 8
+#endif
+constexpr int kSampleShards = FC_SAMPLE_SHARDS;   // k_sample1's global histogram, sharded by workgroup
+constexpr int kCandShards = FC_CAND_SHARDS;       // k_resolve's candidate histogram, likewise
 constexpr int kTickGroups = 16;             // two-level last-arriver tickets (fc_common.h)
 constexpr int kTickStride = 64;             // u32 per ticket counter (one 256-B line each)
 constexpr int kTickWords = (kTickGroups + 1) * kTickStride;
