@@ -1,21 +1,23 @@
 // fc_topk.hip — top-k / native rand-k encode for MI355X (gfx950).
 //
 // Replaces compression.py:31-45 (argsort(|g|)[::-1][:k] / permutation[:k]).  Fast path =
-// three launches, ONE streaming read of g:
+// three stages, ONE streaming read of g (a lone client's sample and compaction share one
+// launch, k_fused_mag):
 //
-//   k_sample1                 stratified sample (<= 1 M keys, < 1 % of g) -> one 4096-bin
+//   k_sample1                 stratified sample (<= 2 M keys, < 2 % of g) -> one 4096-bin
 //                             histogram whose fine window a pilot sub-sample places -> key
 //                             bracket [t_lo, t_hi] around the k-th key (+-6 sigma of the
 //                             sample quantile)
-//   k_compact                 one pass over g, one independent workgroup per 8192-element
+//   k_compact(_mag1)          one pass over g, one independent workgroup per 8192-element
 //                             chunk: every element with key >= t_lo is written (idx, val) in
 //                             ascending index order into the chunk's SLOT of the packet
 //                             ([c*8192, c*8192 + cnt[c])) — no global scan, no look-back; keys
 //                             inside the bracket ("candidates") also go to the chunk's
-//                             candidate slot and a 4096-bin histogram
-//   k_resolve                 histogram -> the bin holding rank r = k - #(key > t_hi);
-//                             gather that bin's candidates; LDS bitonic sort -> exact T64
-//                             (dense output: the same launch then zeroes the slack in q)
+//                             candidate slot (k_fused_mag also bins them: 4096-bin histogram)
+//   k_resolve                 candidate histogram (built here from the candidate slots unless
+//                             k_fused_mag did) -> the bin holding rank r = k - #(key > t_hi);
+//                             gather that bin's candidates; LDS rank / bitonic sort -> exact
+//                             T64 (dense output: the same launch then zeroes the slack in q)
 //
 // Anything unusual (bracket missed, candidate list overflow, > 4096 survivors) sets
 // FC_STATUS_RETRY_EXACT; fc_topk_encode_exact then runs k_engine (12-bit radix select over
@@ -386,8 +388,8 @@ __global__ __launch_bounds__(kBlock) void k_sample1(const float* __restrict__ g,
 // no global scan).  Element layout: e = i*2048 + w*256 + lane*4 + j (i < 4, w < 8, j < 4):
 // each wave instruction moves 1 KiB contiguous and (i, w, lane, j) order is ascending index
 // order, so ballot + mbcnt + a 32-slot LDS scan give ordered offsets inside the chunk's slot.
-// Listed entries are staged in LDS and leave as coalesced 16-B stores; candidate histogram
-// bins are flushed 64 lanes per atomic instruction.
+// Listed entries are staged in LDS and leave as coalesced 16-B stores; candidates go to the
+// chunk's candidate slot (k_resolve bins them).
 // --------------------------------------------------------------------------------------
 enum Pred : int { kPredKey = 0, kPredMask = 1, kPredBern = 2 };
 
