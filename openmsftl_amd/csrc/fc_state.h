@@ -39,7 +39,7 @@ static_assert(sizeof(TopkState) <= 1024, "state block");
 #define FC_SAMPLE_SHARDS 8
 #endif
 #ifndef FC_CAND_SHARDS
-#define FC_CAND_SHARDS 8
+#define FC_CAND_SHARDS 4
 #endif
 constexpr int kSampleShards = FC_SAMPLE_SHARDS;   // k_sample1's global histogram, sharded by workgroup
 constexpr int kCandShards = FC_CAND_SHARDS;       // k_resolve's candidate histogram, likewise

@@ -1339,8 +1339,9 @@ __global__ __launch_bounds__(kBlock) void k_resolve(ResolveArgs a0) {
     }
   };
   // ---- the candidate histogram: every workgroup bins the candidates of its chunk range in
-  // LDS and flushes the non-empty bins into one of kCandShards shards (one shared histogram
-  // queued ~94 same-address atomics per bin at 128 M); the last arriver (two-level ticket)
+  // LDS and flushes the non-empty bins into one of kCandShards (4) shards (one shared
+  // histogram queued ~94 same-address atomics per bin with 256 workgroups; 8 or 16 shards
+  // measured no better for a batch's 16 per client); the last arriver (two-level ticket)
   // sums the shards, finds the bin beta holding rank r and publishes it (generation word
   // hgen).  (The compaction used to add every candidate into the histogram with a global
   // atomic: 5.7 % of that pass at 128 M.)  The wait
