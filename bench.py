@@ -440,7 +440,7 @@ def single_gradient(torch, codec, g, k, n, iters=20):
                             "hbm_frac": round(alg / dt_d / 1e9 / HBM_PEAK_GBPS, 4)}}
 
 
-def small_configs(torch, codec, L, device, f, n=16_777_216, M=128, steps=5):
+def small_configs(torch, codec, L, device, f, n=16_777_216, M=128, steps=20):
     """BASELINE configs[1] (one 16 M gradient: encode + dense decode) and configs[2] (128
     clients x 16 M: batched encode + on-device FedAVG fold), device-resident, same codec."""
     from openmsftl_amd.compression import kept_count
