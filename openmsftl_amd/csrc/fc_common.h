@@ -22,7 +22,10 @@ constexpr int kHistBins = 1 << kHistBits;   // 4096
 constexpr int kSmallCap = 4096;             // exact-finish list (LDS bitonic, 32 KiB)
 constexpr int kEngineGrid = 256;            // radix-engine workgroups (one per CU)
 constexpr int kEnginePasses = 6;            // ceil(63 / 12): enough for any comp width
-constexpr int kResolveGrid = 256;           // k_resolve workgroups
+#ifndef FC_RESOLVE_GRID
+#define FC_RESOLVE_GRID 256
+#endif
+constexpr int kResolveGrid = FC_RESOLVE_GRID;           // k_resolve workgroups
 #ifndef FC_RESOLVE_GRID_BATCH
 #define FC_RESOLVE_GRID_BATCH 16
 #endif
