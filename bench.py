@@ -62,7 +62,45 @@ def parse():
                     help="encode client by client (fc_topk_encode) instead of batched")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r02_pmc_k_compact_mag1.json"),
                     help="PMC summary (profiles/) used for roofline.traffic")
+    ap.add_argument("--force-retry-rank", type=int, default=-1,
+                    help="test only: on this rank, mark client 0's packet RETRY in the last "
+                         "timed step (exercises the rank-uniform exact re-encode)")
+    ap.add_argument("--dump-agg", default=None,
+                    help="test only: rank 0 saves the last step's aggregate (.npy) here")
     return ap.parse_args()
+
+
+def spawn_ranks(argv, nproc):
+    """`bench.py --gpus N` without a launcher: start N ranks (one process per GPU, the env
+    torch.distributed.run would set: RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*) as CHILD
+    processes, before this process touches the GPU, and return the worst exit code (never
+    exec: the parent stays alive and GPU-free).  A rank that fails ends the others."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(nproc):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nproc),
+                   LOCAL_WORLD_SIZE=str(nproc), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv),
+                                      env=env))
+    log(f"[launcher] {nproc} ranks, pids {[p.pid for p in procs]}, port {port}")
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:                      # a failed rank would hang the others
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
 
 
 def log(*a):
@@ -164,13 +202,18 @@ def _packet_equal(torch, p, q):
                 and torch.equal(p.val.view(torch.int32)[listed], q.val.view(torch.int32)[listed]))
 
 
-def self_check(torch, codec, grads, pkts, k):
+def self_check(torch, codec, grads, pkts, k, redone=()):
     """Outside the timed region: clients 0 and 1 re-encoded ALONE (fc_topk_encode) give the
-    batched packets byte for byte, and the same dense result (compression.py:31-37)."""
+    batched packets byte for byte, and the same dense result (compression.py:31-37).  A packet
+    the last step re-encoded exactly (``redone``) lists no bracket slack, so only its dense
+    result is compared."""
     ok = True
     for i in (0, 1):
+        if i >= len(pkts):
+            break
         single = codec.encode_top(grads[i], k)
-        ok = ok and _packet_equal(torch, single, pkts[i])
+        if i not in redone:
+            ok = ok and _packet_equal(torch, single, pkts[i])
         a = codec.decode(single).view(torch.int32)
         b = codec.decode(pkts[i]).view(torch.int32)
         ok = ok and bool(torch.equal(a, b))
@@ -195,12 +238,16 @@ def load_pmc(path):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(sys.argv[1:], args.gpus))
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
     if args.backend == "gloo":
         # rehearsal of the multi-rank path on fewer GPUs than ranks (ranks share devices; the
         # partial sums are staged through host memory, distributed.py); never the measurement
@@ -257,7 +304,9 @@ def main():
 
     pipelined = args.pipeline and not args.no_batch
     w_local = [float(x) for x in w_all[rows.start:rows.stop]]
-    folded = lambda rows_, w_, out_, cont_: None    # noqa: E731 (the fold already ran)
+    folded = lambda rows_, w_, out_, cont_: None    # noqa: E731 (this rank folded already)
+    poke = [False]                                  # --force-retry-rank: mark the next step
+    last_redo = set()                               # clients re-encoded exactly, last step
 
     def step():
         b = nstep[0] & 1
@@ -278,19 +327,26 @@ def main():
             else:                                   # 4 launches for all M clients
                 codec.encode_top_batch(grads, k, packets=pkts, jobs=jobs, check=False,
                                        streams=args.streams)
+            if poke[0]:                             # test only: a bracket "miss" on this rank
+                hdrs[0, 36:40].copy_(torch.tensor([L.FC_STATUS_RETRY_EXACT, 0, 0, 0],
+                                                  dtype=torch.uint8))
+                poke[0] = False
             status_host.copy_(hdrs[:, 36:40], non_blocking=True)   # fc_packet_hdr.status
             encoded.record()
             ready = encoded
-        # this rank's fold (unless pipelined above) + RCCL fp32 reduce to rank 0, queued before
-        # the host waits for the statuses (it queues the next step while the fold runs)
-        works[b] = fedavg.aggregate(folded if pipelined else fold, M * world, accs[b],
-                                    weights=w_all, async_op=True)
+            # this rank's fold is queued before the host waits for the statuses: the host
+            # queues the rest of the step while the fold runs
+            fold(rows, w_local, accs[b], False)
         ready.synchronize()
-        if bool((status_host != 0).any()):          # sampled bracket missed: exact re-encode
-            redo_total[0] += codec.resolve(pkts)    # and fold again (after the first reduce)
-            if works[b] is not None:
-                works[b].wait()
-            works[b] = fedavg.aggregate(fold, M * world, accs[b], weights=w_all, async_op=True)
+        bad = status_host.view(torch.int32).view(-1)
+        last_redo.clear()
+        if bool((bad != 0).any()):                  # sampled bracket missed on THIS rank:
+            last_redo.update(int(i) for i in torch.nonzero(bad).view(-1))
+            redo_total[0] += codec.resolve(pkts)    # exact re-encode (stream-ordered after
+            fold(rows, w_local, accs[b], False)     # the first fold) and fold again from +0
+        # the ONE cross-rank collective of the step, issued after every local re-encode: each
+        # rank issues exactly one reduce per step whatever its statuses were (rank-uniform)
+        works[b] = fedavg.aggregate(folded, M * world, accs[b], weights=w_all, async_op=True)
 
     for _ in range(args.warmup):
         step()
@@ -301,7 +357,8 @@ def main():
     t0 = time.perf_counter()
     with L.KernelTimer(L.FC_TIME_COMPACT | L.FC_TIME_DECODE | L.FC_TIME_ENGINE
                        | L.FC_TIME_SAMPLE) as kt:
-        for _ in range(args.steps):
+        for s in range(args.steps):
+            poke[0] = rank == args.force_retry_rank and s == args.steps - 1
             step()
         torch.cuda.synchronize()
     if world > 1:
@@ -314,8 +371,20 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_step = 1e3 * elapsed / args.steps
+    for wk in works:                                # the last reduces land before any read
+        if wk is not None:
+            wk.wait()
+    torch.cuda.synchronize()
+    if args.dump_agg and rank == 0:
+        import numpy as np
+        np.save(args.dump_agg, accs[(nstep[0] - 1) & 1].cpu().numpy())
+    if world > 1:                                   # exact re-encodes over all ranks
+        t = torch.tensor([redo_total[0]], dtype=torch.int64,
+                         device=device if args.backend == "nccl" else "cpu")
+        dist.all_reduce(t)
+        redo_total[0] = int(t.item())
     # the packets of the last timed step against single-client encodes, before anything reuses them
-    checked = self_check(torch, codec, grads, pkts, k)
+    checked = self_check(torch, codec, grads, pkts, k, last_redo)
     grad_bytes = 4.0 * n * M * world
     value = grad_bytes / (elapsed / args.steps) / 1e9
 

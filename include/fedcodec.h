@@ -130,7 +130,8 @@ int fc_workspace_init(void* ws, size_t ws_bytes, fc_stream_t stream);
  * resolved from the bracket's candidates.  hdr->status == FC_STATUS_RETRY_EXACT means the
  * bracket missed (adversarial / tie-heavy data): call fc_topk_encode_exact with the same
  * arguments.  capacity >= fc_packet_capacity(n); cnt and qoff have fc_num_chunks(n) words
- * (qoff may be NULL: not written, and the packet cannot be folded by fc_decode_accumulate). */
+ * (qoff may be NULL: not written; fc_decode_accumulate then folds the packet by scanning each
+ * chunk's whole slot range per quarter, correct but slower). */
 int fc_topk_encode(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_t seed,
                    uint64_t offset, uint16_t* idx, float* val, uint64_t capacity,
                    uint32_t* cnt, uint64_t* qoff, fc_packet_hdr* hdr, void* ws, size_t ws_bytes,
@@ -204,7 +205,8 @@ int fc_decode_dense(const fc_packet_view* pkt, int format, uint64_t n, void* out
 
 /* ---- FedAVG over packets (aggregation.py:61-63 + gar.py:44), bit-exact fp32 ----------
  * views: DEVICE array of m views (same format), client order = row order of G; FC_FMT_IDXVAL
- * views must carry qoff (each chunk quarter is folded by its own wave, no barriers).
+ * each chunk quarter is folded by its own wave with no barrier, using the views' qoff (a view
+ * without qoff is folded by whole-chunk scans).
  * acc[j] = fl(w_0 * d_0[j]);  acc[j] = fl(acc[j] + fl(w_i * d_i[j])) for i = 1..m-1. */
 int fc_decode_accumulate(const fc_packet_view* views_dev, int m, int format, uint64_t n,
                          float* acc, fc_stream_t stream);
@@ -266,6 +268,9 @@ int fc_qsgd_decode_accumulate(const fc_packet_view* views_dev, int m, uint64_t n
  * fc_mask_dense_f64: codec RAND (mask_bits required: q = keep ? g : +0), DROPOUT_BIASED
  *   (q = g * keep) or DROPOUT_UNBIASED (q = (g * keep) / p), the reference's float64
  *   arithmetic including -0 and NaN (inf * 0); mask_bits NULL = native Philox Bernoulli(p).
+ * fc_mask_dense_f32: the same on a float32 gradient (4-B aligned), promoted exactly: the
+ *   float64 array compression.py:47-60 returns for float32 client.grad, -0.0 included
+ *   (replaces compression.py:51-53 / :58-60 on the drop-in path).
  * fc_weighted_sum_dense_f64: gar.py:44 when G or the weights are float64: rows = DEVICE
  *   array of m row pointers (float32 if rows_f64 == 0, promoted exactly), w = DEVICE
  *   float64[m]; out = +0-started row-order fp64 sum of fl64(g_i * w_i); continue_sum != 0
@@ -275,6 +280,8 @@ int fc_topk_dense_f64(const double* g, uint64_t n, uint64_t k, int key_mode, uin
                       uint64_t offset, double* out, void* ws, size_t ws_bytes,
                       fc_stream_t stream);
 int fc_mask_dense_f64(const double* g, uint64_t n, int codec, const uint32_t* mask_bits, double p,
+                      uint64_t seed, uint64_t offset, double* out, fc_stream_t stream);
+int fc_mask_dense_f32(const float* g, uint64_t n, int codec, const uint32_t* mask_bits, double p,
                       uint64_t seed, uint64_t offset, double* out, fc_stream_t stream);
 int fc_weighted_sum_dense_f64(const void* const* rows, int rows_f64, const double* w, int m,
                               uint64_t n, double* out, int continue_sum, fc_stream_t stream);

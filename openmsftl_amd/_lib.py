@@ -97,6 +97,7 @@ SIGNATURES = {
     "fc_qsgd_decode_accumulate": (_i32, [_vp, _i32, _u64, _vp, _i32, _vp]),
     "fc_topk_dense_f64": (_i32, [_vp, _u64, _u64, _i32, _u64, _u64, _vp, _vp, _sz, _vp]),
     "fc_mask_dense_f64": (_i32, [_vp, _u64, _i32, _vp, _dbl, _u64, _u64, _vp, _vp]),
+    "fc_mask_dense_f32": (_i32, [_vp, _u64, _i32, _vp, _dbl, _u64, _u64, _vp, _vp]),
     "fc_weighted_sum_dense_f64": (_i32, [_vp, _i32, _vp, _i32, _u64, _vp, _i32, _vp]),
     "fc_div_scalar_f64": (_i32, [_vp, _u64, _dbl, _vp]),
     "fc_timing_begin": (_i32, [ctypes.c_uint32]),

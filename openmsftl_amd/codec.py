@@ -222,9 +222,12 @@ class BatchWorkspace:
                 "fc_workspace_init")
 
     @classmethod
-    def get(cls, n: int, m: int, device: torch.device) -> "BatchWorkspace":
+    def get(cls, n: int, m: int, device: torch.device, slot: int = 0) -> "BatchWorkspace":
+        """One workspace per (device, stream, n, slot): ``slot`` = the sub-batch index, so two
+        sub-batches dealt to one stream never share encoder state between a SAMPLE part and
+        its FINISH part."""
         key = (device.index if device.index is not None else torch.cuda.current_device(),
-               torch.cuda.current_stream(device).cuda_stream, n)
+               torch.cuda.current_stream(device).cuda_stream, n, slot)
         ws = cls._cache.get(key)
         if ws is None or ws.m < m:
             ws = cls(n, m, device)
@@ -274,7 +277,8 @@ def encode_top_batch(grads: Sequence[torch.Tensor], k: int, *,
     ``groups``: sub-batch sizes (default: ``streams`` equal parts), dealt to the streams in turn.
     Pipelining (bench.py): ``part`` = FC_PART_SAMPLE or FC_PART_FINISH runs one half of the
     pipeline (fc_topk_encode_batch_part; the same ``groups`` / ``streams`` for both halves, so
-    each sub-batch's halves share a stream and its workspace); ``fork=False``: the forked
+    each sub-batch's halves share a stream and its own workspace, keyed by the sub-batch index
+    even when more sub-batches than streams share one stream); ``fork=False``: the forked
     streams do not wait for the caller's stream first; ``join=False``: the caller's stream does
     not wait for them (the caller orders later work itself)."""
     if not grads:
@@ -335,7 +339,7 @@ def encode_top_batch(grads: Sequence[torch.Tensor], k: int, *,
         lo = 0
         for i, size in enumerate(groups):
             with torch.cuda.stream(sides[i % nside]):
-                ws = BatchWorkspace.get(n, size, dev)
+                ws = BatchWorkspace.get(n, size, dev, slot=i)
                 L.check(lib.fc_topk_encode_batch_part(ctypes.c_void_p(base + lo * job_bytes),
                                                       size, n, k, key_mode, packets[0].capacity,
                                                       _vp(ws.buf), ws.nbytes, part, _stream(dev)),
@@ -392,7 +396,7 @@ def encode_fold_batch(grads: Sequence[torch.Tensor], k: int, weights, out: torch
         side = sides[i]
         with torch.cuda.stream(side):
             side.wait_event(start)
-            ws = BatchWorkspace.get(n, size, dev)
+            ws = BatchWorkspace.get(n, size, dev, slot=i)
             L.check(lib.fc_topk_encode_batch(ctypes.c_void_p(jobs.data_ptr() + lo * jb), size, n, k,
                                              L.FC_KEY_MAGNITUDE, packets[0].capacity, _vp(ws.buf),
                                              ws.nbytes, _stream(dev)), "fc_topk_encode_batch")
@@ -598,18 +602,27 @@ def compress_top_dense_f64(g: torch.Tensor, k: int, *, key_mode: int = L.FC_KEY_
 def mask_dense_f64(g: torch.Tensor, codec: int, *, p: float = 0.5,
                    mask_bits: Optional[torch.Tensor] = None, seed: int = 0, offset: int = 0,
                    out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """'rand' (host permutation mask) and 'dropout-*' on a float64 gradient, with the
-    reference's float64 arithmetic (g * mask, (g * mask) / p): fc_mask_dense_f64."""
-    _require_cuda_f32(g, align=8, dtype=torch.float64)
+    """'rand' (host permutation mask) and 'dropout-*' on a float64 OR float32 gradient, with
+    the reference's float64 arithmetic (g * mask, (g * mask) / p; a float32 g is promoted
+    exactly, as NumPy does): fc_mask_dense_f64 / fc_mask_dense_f32.  Result: float64."""
+    f32 = isinstance(g, torch.Tensor) and g.dtype == torch.float32
+    if f32:
+        _require_cuda_f32(g, align=4)
+    else:
+        _require_cuda_f32(g, align=8, dtype=torch.float64)
     n = g.numel()
     if mask_bits is not None and (mask_bits.dtype != _U32 or not mask_bits.is_cuda
                                   or mask_bits.numel() * 32 < n):
         raise ValueError("mask_bits must be an int32 CUDA tensor of ceil(n/32) words")
     if out is None:
         out = torch.empty(n, dtype=torch.float64, device=g.device)
+    _require_cuda_f32(out, "out", align=8, dtype=torch.float64)
+    if out.numel() != n:
+        raise ValueError("out must have n elements")
     lib = L.load()
-    L.check(lib.fc_mask_dense_f64(_vp(g), n, codec, _vp(mask_bits), float(p), seed, offset,
-                                  _vp(out), _stream(g.device)), "fc_mask_dense_f64")
+    fn = lib.fc_mask_dense_f32 if f32 else lib.fc_mask_dense_f64
+    L.check(fn(_vp(g), n, codec, _vp(mask_bits), float(p), seed, offset, _vp(out),
+               _stream(g.device)), "fc_mask_dense_f32" if f32 else "fc_mask_dense_f64")
     return out
 
 

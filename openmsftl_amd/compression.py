@@ -24,8 +24,8 @@ the reference's exact g * 0 (including -0.0).
 Deliberate, documented deviations:
   * ties in 'top' are broken highest-index-first (= stable argsort reversed); the
     reference's unstable argsort leaves that choice implementation-defined;
-  * for 'dropout-*' a dropped coordinate is +0.0 where the reference writes g*0 (-0.0 for
-    negative g); numerically equal, and inf/NaN inputs still give NaN as in the reference.
+  * none for 'dropout-*': the float64 result is g * mask (/ p) byte for byte, -0.0 for a
+    dropped negative g included (round 3; it used to write +0.0).
 """
 from __future__ import annotations
 
@@ -127,24 +127,15 @@ class Compression:
                     else np.zeros(0, dtype=np.float64))
         g = self._to_device(grad)
         codec_id = L.FC_CODEC_DROPOUT_BIASED if fn == 'dropout-biased' else L.FC_CODEC_DROPOUT_UNBIASED
-        if g.dtype == torch.float64:           # g * mask (/ p) in float64, exactly
-            if host_mask is not None:
-                mask = torch.from_numpy(bitmask_words(host_mask, n, True).view(np.int32)).to(g.device)
-                out = codec.mask_dense_f64(g, codec_id, p=float(p), mask_bits=mask)
-            else:
-                out = codec.mask_dense_f64(g, codec_id, p=float(p), seed=self.seed,
-                                           offset=self._next_offset())
-            return out if on_device else out.cpu().numpy()
+        # the dense float64 q = g * mask (/ p) the reference returns, float32 g promoted
+        # exactly (-0.0 for dropped negative g, NaN for dropped inf/NaN); the packet form of
+        # these codecs is codec.encode_mask (bitmap + kept values) for device folds
         if host_mask is not None:
             mask = torch.from_numpy(bitmask_words(host_mask, n, True).view(np.int32)).to(g.device)
-            pkt = codec.encode_mask(g, codec_id, p=float(p), mask_bits=mask)
+            out = codec.mask_dense_f64(g, codec_id, p=float(p), mask_bits=mask)
         else:
-            pkt = codec.encode_mask(g, codec_id, p=float(p), seed=self.seed,
-                                    offset=self._next_offset())
-        hdr = pkt.header()
-        if hdr.status != L.FC_STATUS_OK:
-            raise L.FedCodecError(f"mask encode status {hdr.status}")
-        out = codec.decode(pkt, dtype=torch.float64)               # reference returns float64
+            out = codec.mask_dense_f64(g, codec_id, p=float(p), seed=self.seed,
+                                       offset=self._next_offset())
         return out if on_device else out.cpu().numpy()
 
     # ------------------------------------------------------------------------------------

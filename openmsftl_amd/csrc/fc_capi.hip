@@ -188,7 +188,9 @@ static int launch_sample(int key_mode, dim3 grid, const float* g, const SamplePl
 }
 
 static int launch_engine(int key_mode, const EngineArgs& base, int passes, hipStream_t s) {
-  if (const char* dbg = getenv("FC_DEBUG_ENGINE_PASSES")) passes = atoi(dbg);  // debugging only
+#ifdef FC_DEBUG_BUILD
+  if (const char* dbg = getenv("FC_DEBUG_ENGINE_PASSES")) passes = atoi(dbg);  // debug builds only
+#endif
   for (int p = 0; p < passes; ++p) {
     TimedLaunch t(FC_TIME_ENGINE, s);
     EngineArgs a = base;
@@ -739,8 +741,11 @@ int fc_topk_dense_f64(const double* g, uint64_t n, uint64_t k, int key_mode, uin
   return FC_OK;
 }
 
-int fc_mask_dense_f64(const double* g, uint64_t n, int codec, const uint32_t* mask_bits, double p,
-                      uint64_t seed, uint64_t offset, double* out, fc_stream_t stream) {
+}  // extern "C"
+
+template <typename T>
+static int mask_dense64(const T* g, uint64_t n, int codec, const uint32_t* mask_bits, double p,
+                        uint64_t seed, uint64_t offset, double* out, fc_stream_t stream) {
   FC_CHECK(g && out, "NULL argument");
   FC_CHECK(n >= 1 && n <= 0xffffffffull, "n=%llu outside [1, 2^32-1]", (unsigned long long)n);
   FC_CHECK(codec == FC_CODEC_DROPOUT_BIASED || codec == FC_CODEC_DROPOUT_UNBIASED ||
@@ -753,10 +758,22 @@ int fc_mask_dense_f64(const double* g, uint64_t n, int codec, const uint32_t* ma
   const int mode = codec == FC_CODEC_RAND ? 0 : codec == FC_CODEC_DROPOUT_BIASED ? 1 : 2;
   hipStream_t s = (hipStream_t)stream;
   TimedLaunch t(FC_TIME_COMPACT, s);
-  hipLaunchKernelGGL(k_mask_dense64, dim3(grid_of(n)), dim3(kBlock), 0, s, g, n, mask_bits,
+  hipLaunchKernelGGL(k_mask_dense64<T>, dim3(grid_of(n)), dim3(kBlock), 0, s, g, n, mask_bits,
                      (uint64_t)thr, seed, offset, mode, p, out);
   FC_LAUNCHED("k_mask_dense64");
   return FC_OK;
+}
+
+extern "C" {
+
+int fc_mask_dense_f64(const double* g, uint64_t n, int codec, const uint32_t* mask_bits, double p,
+                      uint64_t seed, uint64_t offset, double* out, fc_stream_t stream) {
+  return mask_dense64(g, n, codec, mask_bits, p, seed, offset, out, stream);
+}
+
+int fc_mask_dense_f32(const float* g, uint64_t n, int codec, const uint32_t* mask_bits, double p,
+                      uint64_t seed, uint64_t offset, double* out, fc_stream_t stream) {
+  return mask_dense64(g, n, codec, mask_bits, p, seed, offset, out, stream);
 }
 
 int fc_weighted_sum_dense_f64(const void* const* rows, int rows_f64, const double* w, int m,

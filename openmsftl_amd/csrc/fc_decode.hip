@@ -666,15 +666,23 @@ constexpr int kQGroup = FC_QG;                  // items per load group
 // right after its rounds; only a quarter above FC_QTAIL * 64 entries takes the slow body
 constexpr int kQTail = FC_QTAIL > FC_QR ? FC_QTAIL : FC_QR;
 
+static_assert(kSparseMaxM <= 128, "k_fold_q reads the quarter offsets of <= 128 packets "
+                                   "(lanes 0..63 and 64..127)");
+
 struct QMeta {
   const void* idx;                              // uint16 chunk-local indices
   const float* val;
-  const uint64_t* qoff;
+  const void* qoff;                             // quarter offsets, or the counts (kQNoQoff)
   const fc_packet_hdr* hdr;
   uint64_t thresh;
   float w;
   uint32_t flags;                               // ib | codec << 8 | key_mode << 16 | poison << 24
-};
+};                                              //    | kQNoQoff
+// a view without quarter offsets (the encoders may be given qoff = NULL): QMeta::qoff holds the
+// per-chunk counts instead, and the chunk's offsets word becomes kQWhole | cnt — every quarter
+// then scans the whole slot range [0, cnt) (slow body, loc filter), so the fold stays correct
+constexpr uint32_t kQNoQoff = 1u << 25;
+constexpr uint64_t kQWhole = 1ull << 63;        // never set in real offsets (cnt <= 8192)
 
 // One entry of a packet folded into the quarter tile with the full per-entry rules (the slow
 // body): rand-k (Philox keys) slack filter, dropout-unbiased fl32(fl64(v)/p) scaling.
@@ -704,14 +712,15 @@ __global__ __launch_bounds__(kQBlock, 4) void k_fold_q(DecodeArgs a) {
     const fc_packet_view v = a.views[tid];
     const fc_packet_hdr* h = v.hdr;
     QMeta d;
-    d.idx = v.idx; d.val = v.val; d.qoff = v.qoff; d.hdr = h;
+    d.idx = v.idx; d.val = v.val; d.hdr = h;
+    d.qoff = v.qoff ? (const void*)v.qoff : (const void*)v.cnt;
     d.thresh = h->thresh; d.w = v.weight;
     const uint32_t codec = h->codec, key_mode = h->key_mode;
     const float dz = (codec == FC_CODEC_DROPOUT_UNBIASED && h->p == 0.0) ? __uint_as_float(0x7fc00000u) : 0.0f;
     const bool poison = __fmul_rn(dz, v.weight) != __fmul_rn(dz, v.weight);
     const bool generic = codec == FC_CODEC_DROPOUT_UNBIASED || (key_mode == FC_KEY_PHILOX && d.thresh != 0);
     d.flags = (h->index_bits & 0xffu) | ((codec & 0xffu) << 8) | ((key_mode & 0xffu) << 16) |
-              ((uint32_t)poison << 24);
+              ((uint32_t)poison << 24) | (v.qoff ? 0u : kQNoQoff);
     s_meta[tid] = d;
     if (poison || generic) atomicOr(&s_slow, 1u);
   }
@@ -720,12 +729,19 @@ __global__ __launch_bounds__(kQBlock, 4) void k_fold_q(DecodeArgs a) {
   // this chunk's quarter offsets of packets lane and lane + 64
   // (a per-lane pointer: each lane reads a different packet's array)
   typedef __attribute__((address_space(1))) const uint64_t gu64;
-  const uint64_t qo0 = (uint32_t)lane < M ? ((gu64*)s_meta[lane].qoff)[c] : 0ull;
-  const uint64_t qo1 = (uint32_t)lane + 64 < M ? ((gu64*)s_meta[lane + 64].qoff)[c] : 0ull;
+  typedef __attribute__((address_space(1))) const uint32_t gu32c;
+  auto qload = [&](uint32_t m) -> uint64_t {
+    const QMeta& pm = s_meta[m];
+    if (pm.flags & kQNoQoff) return kQWhole | ((gu32c*)pm.qoff)[c];
+    return ((gu64*)pm.qoff)[c];
+  };
+  const uint64_t qo0 = (uint32_t)lane < M ? qload((uint32_t)lane) : 0ull;
+  const uint64_t qo1 = (uint32_t)lane + 64 < M ? qload((uint32_t)lane + 64) : 0ull;
   // a quarter holding more than kQR * 64 entries in any packet sends this wave to the slow
   // body too: the fast body has no tail loop (a load loop inside the pipeline made the
   // compiler wait vmcnt(0) for the other slot's loads)
   auto qcount = [&](uint64_t v) -> uint32_t {
+    if (v & kQWhole) return kQuarter + 1u;                  // whole-chunk scan: slow body
     const uint32_t st = q == 0 ? 0u : (uint32_t)(v >> (16 * (q - 1))) & 0xffffu;
     const uint32_t en = q == 3 ? (uint32_t)(v >> 48) : (uint32_t)(v >> (16 * q)) & 0xffffu;
     return en - st;
@@ -738,6 +754,7 @@ __global__ __launch_bounds__(kQBlock, 4) void k_fold_q(DecodeArgs a) {
     const uint64_t v = ((uint64_t)hi << 32) | lo;
     st = q == 0 ? 0u : (uint32_t)(v >> (16 * (q - 1))) & 0xffffu;
     en = q == 3 ? (uint32_t)(v >> 48) : (uint32_t)(v >> (16 * q)) & 0xffffu;
+    if (v & kQWhole) { st = 0u; en = lo & 0xffffu; }      // no qoff: the whole slot range
   };
   // ---- tile init: +0 (np.sum's start) or the partial sum being continued ----
   float* qt = tile + q * kQuarter;
@@ -764,7 +781,7 @@ __global__ __launch_bounds__(kQBlock, 4) void k_fold_q(DecodeArgs a) {
       const float w = __uint_as_float(uni32(__float_as_uint(pm.w)));
       gu16* pidx = (gu16*)uni_ptr(pm.idx) + base;
       gf32* pval = (gf32*)uni_ptr(pm.val) + base;
-      if (uni32(pm.flags) >> 24) {              // poisoning: NaN where this packet folds nothing
+      if ((uni32(pm.flags) >> 24) & 1u) {       // poisoning: NaN where this packet folds nothing
         for (uint32_t e = st + lane; e < en; e += 64) {
           const uint32_t id = (uint32_t)base + pidx[e];
           const uint32_t loc = id - qbase;

@@ -230,7 +230,10 @@ __device__ __forceinline__ double x86_div(double a, double b) {
 //   mode 0 ('rand'):             q = keep ? g : +0                 (zeros_like + copies)
 //   mode 1 ('dropout-biased'):   q = g * double(keep)              (compression.py:52)
 //   mode 2 ('dropout-unbiased'): q = (g * double(keep)) / p        (compression.py:59-60)
-__global__ __launch_bounds__(kBlock) void k_mask_dense64(const double* __restrict__ g, uint64_t n,
+// T = float: a float32 gradient promoted exactly (NumPy's float32 * int64 mask -> float64), so
+// fp32 'dropout-*' also reproduces g * 0 = -0.0 for negative g and the x86 NaN rules.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_mask_dense64(const T* __restrict__ g, uint64_t n,
                                                          const uint32_t* __restrict__ mask,
                                                          uint64_t bern_thr, uint64_t seed,
                                                          uint64_t off, int mode, double p,
@@ -239,7 +242,7 @@ __global__ __launch_bounds__(kBlock) void k_mask_dense64(const double* __restric
   for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
     const bool keep = mask ? ((mask[i >> 5] >> (i & 31)) & 1u) != 0
                            : (uint64_t)philox_word(i, seed, off) < bern_thr;
-    const double x = g[i];
+    const double x = (double)g[i];
     double q;
     if (mode == 0) {
       q = keep ? x : 0.0;

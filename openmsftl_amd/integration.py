@@ -48,7 +48,7 @@ def install(aggregator: bool = True):
     if "_ref_aggregate_grads" not in cls.__dict__:
         cls._ref_aggregate_grads = cls.aggregate_grads
     cls.aggregate_grads = aggregation.aggregate_grads
-    cls.curr_packets = None
+    cls.agg_path = None
     return ref_agg
 
 

@@ -81,24 +81,72 @@ def test_configs3_shard_shape_8x128M_batched_encode_and_fold():
     _check_batch("configs3")
 
 
-@pytest.mark.timeout(300)
-def test_configs4_host_ring_70x25M():
-    import torch
-    from openmsftl_amd.pipeline import HostFedAvg
+@pytest.fixture(scope="module")
+def configs4_host():
+    """configs[4]'s 70 x 25.5 M client gradients as host NumPy arrays (7.2 GB, made once)."""
     d = D["configs4"]
-    M, n, k = d["clients"], d["n"], d["k"]
     host = []
-    for c in range(M):
+    for c in range(d["clients"]):
         g = MD.fullsize_grad("configs4", c)
         want = d["input_sha256"].get(str(c))
         if want is not None:
             assert sha(g) == want, f"configs4: input generator differs for client {c}"
-        host.append(torch.from_numpy(g).pin_memory())
+        host.append(g)
+    return host
+
+
+@pytest.mark.timeout(300)
+def test_configs4_host_ring_70x25M(configs4_host):
+    import torch
+    from openmsftl_amd.pipeline import HostFedAvg
+    d = D["configs4"]
+    M, n, k = d["clients"], d["n"], d["k"]
+    host = [torch.from_numpy(g).pin_memory() for g in configs4_host]
     pipe = HostFedAvg(n, k, group=d["group"], ring=4)
     out = pipe.run(host, M)
     assert sha(out.numpy()) == d["aggregate_sha256"], "configs4: ring aggregate differs"
     # a second pass over the same pipeline (reused packets and workspaces) gives the same bytes
     assert sha(pipe.run(host, M).numpy()) == d["aggregate_sha256"]
+
+
+class _Client:
+    """The reference Client's fields aggregation.py:54-78 reads (client_id, grad, C)."""
+
+    def __init__(self, cid, grad, C):
+        self.client_id, self.grad, self.C = cid, grad, C
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("pin", ["stage", "register"])
+def test_configs4_device_aggregator_70x25M(configs4_host, pin):
+    """The integrated path driver.py runs: openmsftl_amd.aggregation.Aggregator
+    .aggregate_grads over 70 fake clients whose ``grad`` is a pageable NumPy array
+    (client.py:53), top f = 0.01 (aggregation.py:54-78 -> gar.py:44), NumPy in, NumPy
+    ``agg_grad`` out.  Streamed through the bounded host ring (pinned staging, or the arrays
+    page-locked in place) in fold groups of 64: equal to the oracle's aggregate digest.
+    Prints the NumPy-to-NumPy rate."""
+    import time
+
+    import torch
+    from openmsftl_amd import Compression
+    from openmsftl_amd.aggregation import Aggregator
+    d = D["configs4"]
+    C = Compression({"compression_function": "top", "fraction_coordinate": d["fraction"]})
+    clients = [_Client(i, g, C) for i, g in enumerate(configs4_host)]
+    agg = Aggregator({"aggregation_scheme": "fed_avg"})
+    agg._host_pipelines = {}
+    agg.aggregate_grads(clients)                       # allocates the ring + packets
+    agg._host_pipelines[next(iter(agg._host_pipelines))].pin = pin
+    assert agg.agg_path == "stream-top"
+    assert sha(agg.agg_grad) == d["aggregate_sha256"], "configs4: Aggregator aggregate differs"
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    agg.aggregate_grads(clients)                       # weights persisted (gar.py:41-42)
+    dt = time.perf_counter() - t0
+    assert sha(agg.agg_grad) == d["aggregate_sha256"]
+    gbps = 4.0 * d["n"] * d["clients"] / dt / 1e9
+    print(f"\n[configs4 Aggregator numpy->numpy pin={pin}] {dt:.3f} s = {gbps:.2f} GB/s "
+          f"of client gradients")
 
 
 @pytest.mark.timeout(300)

@@ -1,9 +1,10 @@
 """GPU parity: the HIP codec (through the C ABI) against the CPU oracle / reference goldens.
 
 Run on an MI355X:  python -m pytest tests -m gpu -x -q
-Bars: index sets and top/rand values bit-exact; dropout values equal as the reference's
-consumers see them (assert_array_equal: NaN==NaN, +0==-0) and bit-exact on every nonzero
-finite coordinate; FedAVG bit-exact fp32.
+Bars: index sets and top/rand values bit-exact; the dense dropout result compress() returns
+byte-exact (float64, -0.0 and NaN bits included); dropout packets (bitmap + kept values) equal
+as the reference's consumers see them (assert_array_equal: NaN==NaN, +0==-0) and bit-exact on
+every nonzero finite coordinate; FedAVG bit-exact fp32.
 """
 import hashlib
 
@@ -353,6 +354,27 @@ def test_batch_encode_in_two_parts(streams):
         codec.encode_top_batch(grads, k, packets=pk, part=L.FC_PART_SAMPLE)   # check=True
 
 
+def test_batch_encode_parts_more_groups_than_streams():
+    """Three sub-batches on two streams (group 2 shares stream 0 with group 0): every
+    sub-batch keeps its own encoder state between its SAMPLE and FINISH parts, so no packet
+    comes back RETRY and all equal the one-call encode."""
+    from openmsftl_amd import _lib as L
+    codec = _codec()
+    n, M = 200_003, 7
+    rng = np.random.default_rng(78)
+    grads = [torch.from_numpy((rng.standard_normal(n) * 10.0 ** rng.uniform(-4, 1))
+                              .astype(np.float32)).cuda() for _ in range(M)]
+    k = co.num_kept(0.1, n)
+    want = [_packet_bytes(p) for p in codec.encode_top_batch(grads, k, streams=1)]
+    pk = [codec.Packet.alloc(n, L.FC_FMT_IDXVAL, grads[0].device, k=k) for _ in range(M)]
+    for part in (L.FC_PART_SAMPLE, L.FC_PART_FINISH):
+        codec.encode_top_batch(grads, k, packets=pk, check=False, streams=2, groups=[3, 2, 2],
+                               part=part)
+    torch.cuda.synchronize()
+    assert [int(h.status) for h in codec.headers(pk)] == [0] * M
+    assert [_packet_bytes(p) for p in pk] == want
+
+
 @pytest.mark.parametrize("M,n", [(65, 20_000), (70, 8_193 * 3), (130, 9_000)])
 def test_batch_encode_client_interleave(M, n):
     """k_compact_mag1 interleaves the chunks of 64 clients in dispatch order: a full group, a
@@ -509,7 +531,38 @@ def test_dropout_numpy_rng_golden(name):
     out = Compression({"compression_function": m["codec"], "dropout_p": m["p"]}).compress(g)
     if "rng_next" in m:
         assert int(np.random.randint(0, 2**31 - 1)) == m["rng_next"]
-    _dropout_equal(out, G.arr(name, "output"))
+    ref = G.arr(name, "output")
+    _dropout_equal(out, ref)
+    assert out.tobytes() == ref.tobytes()                     # -0.0 and NaN bits too
+
+
+@pytest.mark.parametrize("codec_name", ["dropout-biased", "dropout-unbiased"])
+@pytest.mark.parametrize("p", [0.1, 0.3, 0.0])
+def test_dropout_dense_f32_byte_exact(codec_name, p):
+    """compress()'s dense fp32 dropout path (fc_mask_dense_f32): g * mask (/ p) in float64,
+    byte for byte as NumPy computes it (compression.py:52, :59) with -0.0 for dropped
+    negative g and NaN for dropped +-inf, on both mask sources."""
+    codec = _codec()
+    L = _L()
+    n = 1_000_003
+    g = np.random.default_rng(12).standard_normal(n, dtype=np.float32)
+    g[::9973] = np.inf
+    g[5::9973] = -np.inf
+    g[7::10007] = np.float32(-0.0)
+    cid = L.FC_CODEC_DROPOUT_BIASED if codec_name == "dropout-biased" else L.FC_CODEC_DROPOUT_UNBIASED
+    gd = torch.from_numpy(g).cuda()
+    out = codec.mask_dense_f64(gd, cid, p=p, seed=9, offset=4).cpu().numpy()
+    mask = ph.bernoulli_mask(n, p, 9, 4).astype(np.int64)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        ref = g * mask if codec_name == "dropout-biased" else (g * mask) / p
+    assert out.tobytes() == ref.tobytes()
+    from openmsftl_amd.compression import bitmask_words
+    hm = np.random.default_rng(3).binomial(1, 0.5, n)
+    mb = torch.from_numpy(bitmask_words(hm, n, True).view(np.int32)).cuda()
+    out = codec.mask_dense_f64(gd, cid, p=p, mask_bits=mb).cpu().numpy()
+    with np.errstate(invalid="ignore", divide="ignore"):
+        ref = g * hm if codec_name == "dropout-biased" else (g * hm) / p
+    assert out.tobytes() == ref.tobytes()
 
 
 @pytest.mark.parametrize("codec_name", ["dropout-biased", "dropout-unbiased"])
@@ -557,6 +610,28 @@ def test_fedavg_packets_bit_exact(M, n, f):
                                         "fraction_coordinate": f}, x) for x in grads], np.float32)
     ref = go.FedAvgOracle({}).aggregate(Gd)
     assert agg.tobytes() == ref.tobytes()
+
+
+def test_fedavg_packets_without_qoff():
+    """include/fedcodec.h: an encoder given qoff = NULL writes no quarter offsets; the fold
+    then scans each chunk's whole slot range per quarter and is still bit-exact (ADVICE r02:
+    it used to dereference the NULL pointer).  Mixed with packets that do carry qoff."""
+    codec = _codec()
+    M, n, f = 5, 70_001, 0.1
+    rng = np.random.default_rng(505)
+    grads = [(rng.standard_normal(n) * 10.0 ** rng.uniform(-4, -1)).astype(np.float32)
+             for _ in range(M)]
+    k = co.num_kept(f, n)
+    pkts = []
+    for i, x in enumerate(grads):
+        p = codec.Packet.alloc(n, 0, "cuda", k=k)
+        if i % 2 == 0:
+            p.qoff = None                                          # encoded with qoff = NULL
+        pkts.append(codec.encode_top(torch.from_numpy(x).cuda(), k, packet=p))
+    agg = codec.decode_accumulate(pkts, list(np.full(M, 1.0 / M, np.float32))).cpu().numpy()
+    Gd = go.build_dense_G([co.compress({"compression_function": "top",
+                                        "fraction_coordinate": f}, x) for x in grads], np.float32)
+    assert agg.tobytes() == go.FedAvgOracle({}).aggregate(Gd).tobytes()
 
 
 @pytest.mark.parametrize("split", [1, 5, 70])
@@ -715,8 +790,9 @@ def test_aggregator_hierarchical_golden(name):
 
 @pytest.mark.parametrize("sizes", [[], [3], [4, 2]])
 def test_aggregator_top_packets_match_dense_reference(sizes):
-    """The packet path (batched top-k encode, packet fold / packet cluster means) == the dense
-    G the reference builds from the same compressed rows, merged and reduced (oracle)."""
+    """The streamed packet path (host ring -> top-k encode -> packet fold / packet cluster
+    means) == the dense G the reference builds from the same compressed rows, merged and
+    reduced (oracle).  A budget of a few packets forces several fold groups per cluster."""
     from openmsftl_amd.aggregation import Aggregator
     M, n, f = 17, 40_961, 0.1
     rng = np.random.default_rng(len(sizes))
@@ -726,10 +802,12 @@ def test_aggregator_top_packets_match_dense_reference(sizes):
     for x in grads[:3]:
         x[:100] = -0.0                               # signed zeros in the kept set
     clients = [_Client(i, g, cfg) for i, g in enumerate(grads)]
+    from openmsftl_amd.pipeline import packet_bytes
     agg = Aggregator({"aggregation_scheme": "fed_avg", "num_hierarchies": len(sizes),
-                      "cluster_size_list": sizes})
+                      "cluster_size_list": sizes,
+                      "device_budget_bytes": 6 * 4 * n + 3 * packet_bytes(n) + (8 << 20)})
     agg.aggregate_grads(clients)
-    assert agg.curr_packets is not None                # the packet path ran
+    assert agg.agg_path == "stream-top"                # the streamed packet path ran
     Gd = go.build_dense_G([co.compress(cfg, x) for x in grads], np.float32)
     for cs in sizes:
         Gd = go.merge_gradient(Gd, cs)
