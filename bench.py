@@ -55,6 +55,8 @@ def parse():
                     help="nccl (RCCL over xGMI: the measurement) or gloo (rehearsal only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-single", action="store_true", help="skip the single-gradient probe")
+    ap.add_argument("--no-matrix", action="store_true",
+                    help="skip the SURVEY §8(d) codec matrix (extra.codec_matrix)")
     ap.add_argument("--pipeline", action="store_true",
                     help="fold each encode chain's packets on its stream as soon as they are "
                          "encoded (codec.encode_fold_batch; measured no faster, A/B only)")
@@ -443,6 +445,8 @@ def main():
     torch.cuda.empty_cache()
     if world == 1 and rank == 0 and not args.no_single:
         extra["configs_1_2"] = small_configs(torch, codec, L, device, f)
+    if world == 1 and rank == 0 and not args.no_matrix:
+        extra["codec_matrix"] = codec_matrix(torch, codec, L, device)
 
     cpu = None
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
@@ -542,6 +546,107 @@ def small_configs(torch, codec, L, device, f, n=16_777_216, M=128, steps=20):
                                 "alg_GBps": round(alg / dt / 1e9, 1),
                                 "hbm_frac": round(alg / dt / 1e9 / HBM_PEAK_GBPS, 4),
                                 "exact_fallbacks": redo}}
+
+
+def _time_us(torch, fn, iters=20, warm=3):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / iters * 1e6
+
+
+def _row(us, alg, **kw):
+    return {"us": round(us, 1), "alg_bytes": int(alg), "alg_GBps": round(alg / us / 1e3, 1),
+            "hbm_frac": round(alg / us / 1e3 / HBM_PEAK_GBPS, 4), **kw}
+
+
+def codec_matrix(torch, codec, L, device, n16=16_777_216, n25=25_557_032):
+    """SURVEY.md §8(d)'s other codec settings, device-resident, encode + decode of one gradient
+    (the `roofline` algorithmic bytes of §8(d): top/rand packets 8N + 16k; dropout bitmap
+    packets 2 (4N + N/8 + 4 nnz); the dense drop-in results read 4N and write the dense q;
+    'full' FedAVG M 4N + 4N).  Host RNG draws (np.random, parity mode) happen before timing:
+    only their device work (mask -> packet -> dense) is timed."""
+    import numpy as np
+    from openmsftl_amd.compression import bitmask_words, kept_count
+    rows = {}
+    gen = torch.Generator(device=device)
+    g16 = torch.randn(n16, device=device, generator=gen.manual_seed(5)).mul_(1e-2)
+    out16 = torch.empty_like(g16)
+    # top f = 0.01 (configs[4]'s codec) at 16 M and 25.5 M: packet encode + decode, and the
+    # drop-in dense path (k_fused_mag<true> + k_resolve)
+    for name, n in (("top_f0.01_16M", n16), ("top_f0.01_25.5M", n25)):
+        g = g16 if n == n16 else torch.randn(n, device=device, generator=gen.manual_seed(6)).mul_(1e-2)
+        out = out16 if n == n16 else torch.empty_like(g)
+        k = kept_count(0.01, n)
+        pkt = codec.encode_top(g, k)
+        us = _time_us(torch, lambda: (codec.encode_top(g, k, packet=pkt, check=False),
+                                      codec.decode(pkt, out=out)))
+        usd = _time_us(torch, lambda: codec.compress_top_dense(g, k, out=out, packet=pkt, check=False))
+        assert codec.resolve([pkt]) == 0
+        alg = 8.0 * n + 16.0 * k
+        rows[name] = _row(us, alg, n=n, k=k, path="fc_topk_encode + fc_decode_dense",
+                          dense=_row(usd, alg, path="fc_topk_encode_dense"))
+    # rand f = 0.1 at 16 M: native Philox keys (fc_topk_encode PHILOX) and parity mode (the
+    # host permutation as a bit mask -> fc_mask_encode idx/val -> decode)
+    k = kept_count(0.1, n16)
+    pkt = codec.encode_top(g16, k, key_mode=L.FC_KEY_PHILOX, seed=3, offset=1)
+    us = _time_us(torch, lambda: (codec.encode_top(g16, k, key_mode=L.FC_KEY_PHILOX, seed=3, offset=1,
+                                                   packet=pkt, check=False),
+                                  codec.decode(pkt, out=out16)))
+    assert codec.resolve([pkt]) == 0
+    rows["rand_f0.1_16M_philox"] = _row(us, 8.0 * n16 + 16.0 * k, n=n16, k=k,
+                                        path="fc_topk_encode(PHILOX) + fc_decode_dense")
+    idx = np.random.default_rng(1).permutation(n16)[:k]
+    mask = torch.from_numpy(bitmask_words(idx, n16, False).view(np.int32)).to(device)
+    pm = codec.encode_mask(g16, L.FC_CODEC_RAND, mask_bits=mask, fmt=L.FC_FMT_IDXVAL)
+    us = _time_us(torch, lambda: (codec.encode_mask(g16, L.FC_CODEC_RAND, mask_bits=mask,
+                                                    fmt=L.FC_FMT_IDXVAL, packet=pm),
+                                  codec.decode(pm, out=out16)))
+    rows["rand_f0.1_16M_hostmask"] = _row(us, 8.0 * n16 + 16.0 * k + n16 / 8.0, n=n16, k=k,
+                                          path="fc_mask_encode(RAND, idx/val) + fc_decode_dense; "
+                                               "alg + N/8 mask bytes")
+    # dropout p = 0.1 (client_config.json:49), both codecs, both mask sources: bitmap packet
+    # encode + dense decode, and the drop-in dense float64 q (fc_mask_dense_f32)
+    hm = np.random.default_rng(2).binomial(1, 0.1, n16)
+    mb = torch.from_numpy(bitmask_words(hm, n16, True).view(np.int32)).to(device)
+    out64 = torch.empty(n16, dtype=torch.float64, device=device)
+    for cname, cid in (("dropout-biased", L.FC_CODEC_DROPOUT_BIASED),
+                       ("dropout-unbiased", L.FC_CODEC_DROPOUT_UNBIASED)):
+        for src, kw in (("philox", {"seed": 4, "offset": 2}), ("hostmask", {"mask_bits": mb})):
+            pb = codec.encode_mask(g16, cid, p=0.1, **kw)
+            us = _time_us(torch, lambda: (codec.encode_mask(g16, cid, p=0.1, packet=pb, **kw),
+                                          codec.decode(pb, out=out16)))
+            nnz = int(pb.cnt.sum().item())
+            alg = 2.0 * (4.0 * n16 + n16 / 8.0 + 4.0 * nnz)
+            usd = _time_us(torch, lambda: codec.mask_dense_f64(g16, cid, p=0.1, out=out64, **kw))
+            algd = 4.0 * n16 + 8.0 * n16 + (n16 / 8.0 if src == "hostmask" else 0.0)
+            rows[f"{cname}_p0.1_16M_{src}"] = _row(
+                us, alg, n=n16, nnz=nnz, path="fc_mask_encode(bitmap) + fc_decode_dense",
+                dense_f64=_row(usd, algd, path="fc_mask_dense_f32 (drop-in float64 q)"))
+    # 'full' (compression.py:27-29 returns g itself): FedAVG of 128 x 16 M dense rows (k_wsum)
+    M = 128
+    G = torch.randn((M, n16), device=device, generator=gen.manual_seed(7))
+    w = torch.full((M,), 1.0 / M, dtype=torch.float32)
+    acc = torch.empty(n16, dtype=torch.float32, device=device)
+    rows_l = list(G.unbind(0))
+    us = _time_us(torch, lambda: codec.weighted_sum_dense(rows_l, w, out=acc), iters=10)
+    rows["full_fedavg_128x16M"] = _row(us, M * 4.0 * n16 + 4.0 * n16, clients=M, n=n16,
+                                       path="fc_weighted_sum_dense (k_wsum)")
+    del G, rows_l
+    # float64 gradient, top f = 0.1 at 16 M (RandomGaussian noise_scale 0 hands float64 over)
+    g64 = g16.double()
+    o64 = torch.empty_like(g64)
+    k = kept_count(0.1, n16)
+    us = _time_us(torch, lambda: codec.compress_top_dense_f64(g64, k, out=o64), iters=10)
+    rows["top_f0.1_16M_fp64"] = _row(us, 16.0 * n16, n=n16, k=k,
+                                     path="fc_topk_dense_f64 (exact radix select, <= 8 passes); "
+                                          "alg = read 8N + write 8N")
+    torch.cuda.empty_cache()
+    return rows
 
 
 def qsgd_single(torch, codec, g, n, bits=2, iters=20):

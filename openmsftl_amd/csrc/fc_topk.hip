@@ -593,16 +593,7 @@ __global__ __launch_bounds__(kCBlock, FC_COMPACT_WAVES_PER_EU) void k_compact(Co
 
   const uint32_t tot_e = s_tot[0];
   const uint64_t slot = base;                     // entries slot of this chunk
-#ifdef FC_ABLATE
-  asm volatile("" ::"v"(pbits), "v"(cbits), "v"(x01), "v"(x23));   // diagnostic build only
-  if (FC_ABLATE == 1) return;
-#endif
-#ifdef FC_ABLATE
-  constexpr bool kAblCand = FC_ABLATE == 2, kAblCopy = FC_ABLATE == 3, kAblStage = FC_ABLATE == 4;
-#else
-  constexpr bool kAblCand = false, kAblCopy = false, kAblStage = false;
-#endif
-  if (tot_e <= (uint32_t)kStage && !kAblStage) {  // block-uniform: stage in LDS
+  if (tot_e <= (uint32_t)kStage) {                // block-uniform: stage in LDS
     // LDS store cost is per wave instruction, not per active lane: instead of one store per
     // element (32 per thread, ~1 GB of LDS traffic per 128M launch) each float4 runs only as
     // many rounds as its busiest lane has listed elements (~2 at f = 0.1), one b64 per round.
@@ -610,7 +601,7 @@ __global__ __launch_bounds__(kCBlock, FC_COMPACT_WAVES_PER_EU) void k_compact(Co
     stage_f4<PRED>(st, x[1], pbits >> 4, cbits >> 4, s_ent[1 * kCWaves + w] + (x01 >> 16), 1 * 2048 + w * 256 + lane * 4, lane);
     stage_f4<PRED>(st, x[2], pbits >> 8, cbits >> 8, s_ent[2 * kCWaves + w] + (x23 & 0xffffu), 2 * 2048 + w * 256 + lane * 4, lane);
     stage_f4<PRED>(st, x[3], pbits >> 12, cbits >> 12, s_ent[3 * kCWaves + w] + (x23 >> 16), 3 * 2048 + w * 256 + lane * 4, lane);
-  } else if (!kAblStage) {                        // dense chunk: direct (predicated) stores
+  } else {                                        // dense chunk: direct (predicated) stores
 #pragma unroll
     for (int i = 0; i < kCVec; ++i) {
       const uint32_t e0 = base + (uint32_t)(i * 2048 + w * 256 + lane * 4);
@@ -628,7 +619,7 @@ __global__ __launch_bounds__(kCBlock, FC_COMPACT_WAVES_PER_EU) void k_compact(Co
       }
     }
   }
-  if (wave_cand && !kAblCand) {                    // candidates: rare, predicated
+  if (wave_cand) {                                // candidates: rare, predicated
     const uint64_t cslot = (uint64_t)chunk * kCandSlot;
 #pragma unroll
     for (int i = 0; i < kCVec; ++i) {
@@ -651,7 +642,7 @@ __global__ __launch_bounds__(kCBlock, FC_COMPACT_WAVES_PER_EU) void k_compact(Co
     }
   }
   __syncthreads();
-  if (tot_e <= (uint32_t)kStage && !kAblCopy) {   // coalesced 16-B stores of the staged slot
+  if (tot_e <= (uint32_t)kStage) {                // coalesced 16-B stores of the staged slot
     for (uint32_t t = 4 * tid; t < tot_e; t += 4 * kCBlock) {
       if (t + 4 <= tot_e) {
         const uint4 p0 = *reinterpret_cast<const uint4*>(&st[t]);
@@ -861,11 +852,7 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
   // encode chain but not on a lone client's critical path).
   constexpr int kCW = kCandSlot / NW;
   uint32_t wc = 0;
-#ifdef FC_ABL_CAND                                    // timing-only ablation (wrong results)
-  if (false) {
-#else
   if (P.cand_on) {
-#endif
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const bool c = mag_cand<FAST>(P, x[q]);
