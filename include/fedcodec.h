@@ -66,6 +66,8 @@ typedef void* fc_stream_t; /* hipStream_t */
 #define FC_FMT_IDXVAL 0      /* uint16 idx[] (chunk-local, ascending) + float val[] */
 #define FC_FMT_BITMAP 1      /* uint32 bitmap[ceil(N/8192)*256] + float val[] */
 #define FC_FMT_QSGD 2        /* packed W-bit codes (sign | level), fc_qsgd_code_words */
+#define FC_FMT_DENSE 3       /* header of fc_topk_encode_dense: the dense q is the product;
+                                idx/val/cnt/qoff are scratch (not a decodable packet) */
 
 /* Slotted packet layout: the gradient is cut into chunks of FC_CHUNK elements; chunk c's
  * entries (ascending index order) live at [c*FC_CHUNK, c*FC_CHUNK + cnt[c]) of idx/val (and
@@ -138,10 +140,12 @@ int fc_topk_encode(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_
                    fc_stream_t stream);
 /* ---- top-k straight to the dense result (compression.py:31-37 returns q, not a packet) --
  * The fc_topk_encode pipeline (magnitude keys) whose compaction pass also streams
- * q = zeros_like(g); q[listed] = g into `dense` (n floats, 16-B aligned), then a fix-up
- * launch zeroes the slack entries once T64 is known.  The packet is written as usual.  If the
- * header reports FC_STATUS_RETRY_EXACT, `dense` is not valid: re-encode with
- * fc_topk_encode_exact and fc_decode_dense (as for a packet).  Needs 0 < k < n. */
+ * q = zeros_like(g); q[listed] = g into `dense` (n floats, 16-B aligned); the resolve zeroes
+ * the slack entries once T64 is known.  q is the product: the packet buffers are scratch (the
+ * entries are written only for chunks the resolve has to re-read) and the header's format is
+ * FC_FMT_DENSE (thresh / status valid; not decodable).  If the header reports
+ * FC_STATUS_RETRY_EXACT, `dense` is not valid: re-encode with fc_topk_encode_exact (a full
+ * packet) and fc_decode_dense.  Needs 0 < k < n. */
 int fc_topk_encode_dense(const float* g, uint64_t n, uint64_t k, uint16_t* idx, float* val,
                          uint64_t capacity, uint32_t* cnt, uint64_t* qoff, fc_packet_hdr* hdr,
                          void* ws, size_t ws_bytes, float* dense, fc_stream_t stream);

@@ -18,7 +18,7 @@ FC_STATUS_OK, FC_STATUS_RETRY_EXACT, FC_STATUS_OVERFLOW, FC_STATUS_TIMEOUT = 0, 
 FC_CODEC_TOP, FC_CODEC_RAND, FC_CODEC_DROPOUT_BIASED, FC_CODEC_DROPOUT_UNBIASED = 1, 2, 3, 4
 FC_CODEC_QSGD = 5
 FC_KEY_MAGNITUDE, FC_KEY_PHILOX = 0, 1
-FC_FMT_IDXVAL, FC_FMT_BITMAP, FC_FMT_QSGD = 0, 1, 2
+FC_FMT_IDXVAL, FC_FMT_BITMAP, FC_FMT_QSGD, FC_FMT_DENSE = 0, 1, 2, 3
 FC_PART_SAMPLE, FC_PART_FINISH = 1, 2
 FC_CHUNK = 8192
 HDR_BYTES = 96

@@ -109,7 +109,13 @@ class Packet:
         :func:`resolve` has seen the packet OK), so the gradient's memory can be reused."""
         self._enc = None
 
+    def _decodable(self) -> None:
+        if getattr(self, "_dense_only", False):
+            raise ValueError("this packet was scratch of compress_top_dense (header format "
+                             "FC_FMT_DENSE): it lists no entries; decode the dense q instead")
+
     def view(self, weight: float = 1.0) -> L.PacketView:
+        self._decodable()
         return L.PacketView(idx=self.idx.data_ptr() if self.idx is not None else 0,
                             val=self.val.data_ptr(),
                             bitmap=self.bitmap.data_ptr() if self.bitmap is not None else 0,
@@ -126,6 +132,7 @@ class Packet:
         """(idx uint32 = global element index, val float32, header) of every LISTED entry,
         ascending — includes the sampled-bracket slack (comp < thresh); inspection / test
         helper (synchronises)."""
+        self._decodable()
         h = self.header()
         cnt = self.cnt.cpu().numpy().astype(np.int64)
         pos = np.arange(self.capacity, dtype=np.int64)
@@ -171,6 +178,7 @@ def encode_top(g: torch.Tensor, k: int, *, key_mode: int = L.FC_KEY_MAGNITUDE, s
                packet.capacity, _vp(packet.cnt), _vp(packet.qoff), _vp(packet.hdr), _vp(ws.buf),
                ws.nbytes, _stream(g.device)), "fc_topk_encode")
     packet._enc = (g, k, key_mode, seed, offset)
+    packet._dense_only = False
     if check:
         resolve([packet])
     return packet
@@ -179,9 +187,10 @@ def encode_top(g: torch.Tensor, k: int, *, key_mode: int = L.FC_KEY_MAGNITUDE, s
 def compress_top_dense(g: torch.Tensor, k: int, out: Optional[torch.Tensor] = None,
                        packet: Optional[Packet] = None, check: bool = True) -> torch.Tensor:
     """compression.py:31-37 on the device, straight to the dense q (fc_topk_encode_dense):
-    the compaction pass streams q while it lists the packet, a fix-up zeroes the slack.
-    Same bytes as ``decode(encode_top(g, k))``.  ``check=False`` skips the status read (call
-    :func:`resolve` + :func:`decode` yourself if the header reports a retry)."""
+    one pass streams q (the packet buffers are scratch: no entries are written, the header
+    says FC_FMT_DENSE), the resolve zeroes the slack.  Same bytes as
+    ``decode(encode_top(g, k))``.  ``check=False`` skips the status read (call :func:`resolve`
+    — it re-encodes a full packet — + :func:`decode` yourself if the header reports a retry)."""
     _require_cuda_f32(g)
     n = g.numel()
     if not 0 <= k <= n:
@@ -203,6 +212,7 @@ def compress_top_dense(g: torch.Tensor, k: int, out: Optional[torch.Tensor] = No
                                      _vp(packet.hdr), _vp(ws.buf), ws.nbytes, _vp(out),
                                      _stream(g.device)), "fc_topk_encode_dense")
     packet._enc = (g, k, L.FC_KEY_MAGNITUDE, 0, 0)
+    packet._dense_only = True
     if check and resolve([packet]):            # bracket missed: exact packet, then decode
         decode(packet, out=out)
     return out
@@ -308,6 +318,7 @@ def encode_top_batch(grads: Sequence[torch.Tensor], k: int, *,
             raise ValueError("packet too small or not idx/val")
         p.k = k
         p._enc = (g, k, key_mode, s, o)
+        p._dense_only = False
     if jobs is None:
         jobs = encode_jobs(grads, packets, seeds, offsets)
     nside = max(1, min(int(streams), m, _MAX_SIDE))
@@ -444,6 +455,7 @@ def resolve(packets: Sequence[Packet]) -> int:
                                          _vp(p.qoff), _vp(p.hdr), _vp(ws.buf), ws.nbytes,
                                          _stream(g.device)), "fc_topk_encode_exact")
         redo += 1
+        p._dense_only = False                        # a full packet now
         h2 = p.header()
         if h2.status != L.FC_STATUS_OK:
             raise L.FedCodecError(f"exact encode status {h2.status}")

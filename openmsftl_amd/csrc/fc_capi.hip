@@ -359,6 +359,7 @@ int fc_topk_encode(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_
   if (key_mode == FC_KEY_MAGNITUDE && fused_enabled()) {
     rc = launch_fused(ca, P, hi, sgrid, s);
     if (rc) return rc;
+    ra.rbin = FC_FUSED_BIN_PKT ? 0u : 1u;
     return launch_resolve(ra, s);
   }
   rc = launch_sample(key_mode, dim3(sgrid), g, P, seed, offset, ca.W, ca.ib, hdr, hi, nullptr, 0ull, s);
@@ -380,12 +381,17 @@ int fc_topk_encode_dense(const float* g, uint64_t n, uint64_t k, uint16_t* idx, 
                      ws_bytes, &ca, &ea, &ra, &hi);
   if (rc) return rc;
   ca.dense = dense;
+  if (fused_enabled() && !FC_DENSE_PKT) {   // q is the product: the header says no entries
+    hi.format = FC_FMT_DENSE;
+    ca.HI.format = FC_FMT_DENSE;
+  }
   hipStream_t s = (hipStream_t)stream;
   const SamplePlan P = make_plan(n, k, true);
   const uint32_t sgrid = (P.nseg + kSampleSegs - 1) / kSampleSegs;
   if (fused_enabled()) {
     rc = launch_fused(ca, P, hi, sgrid, s);
     if (rc) return rc;
+    ra.rbin = FC_FUSED_BIN_DENSE ? 0u : 1u;
   } else {
     ra.rbin = 1;
     rc = launch_sample(FC_KEY_MAGNITUDE, dim3(sgrid), g, P, 0ull, 0ull, ca.W, ca.ib, hdr, hi, nullptr, 0ull, s);

@@ -761,7 +761,10 @@ struct MagOut {
   float* dense;             // nullptr unless fc_topk_encode_dense
 };
 
-template <bool FAST, typename SH, int NW, bool DENSE, bool BIN>
+// PKT = false (the drop-in dense path, fc_topk_encode_dense): q is the product, the packet
+// entries are not written (-6 B per listed element of HBM writes) except for a chunk whose
+// candidates overflowed their slot (k_resolve re-reads that chunk's entries).
+template <bool FAST, typename SH, int NW, bool DENSE, bool BIN, bool PKT = true>
 __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred& P,
                                                  float (&x)[MagGeo<NW>::kQ], SH& sh,
                                                  uint32_t chunk, uint32_t sbin) {
@@ -822,15 +825,9 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
     const float v = p ? (FAST ? x[q] : a.g[e]) : 0.0f;
     __builtin_nontemporal_store(v, a.dense + e);   // (sc1 / plain stores: 269 vs 192 us)
   };
-  if (tot_e <= (uint32_t)SH::kStageN) {                 // block-uniform
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const bool p = mag_listed<FAST>(P, x[q]);
-      const uint32_t pos = prefix_count(__ballot(p)) + goff_of(q);
-      if (p) sh.st[pos] = make_uint2(FC_LOC(q), __float_as_uint(FAST ? x[q] : a.g[base + FC_LOC(q)]));
-      dense_out(q, p);
-    }
-  } else {
+  // entries straight to the chunk's slot (predicated stores): a chunk too dense for the LDS
+  // stage, or (!PKT) one whose candidates overflowed
+  auto direct_entries = [&](bool dense_too) {
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const bool p = mag_listed<FAST>(P, x[q]);
@@ -839,8 +836,22 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
         a.idx[slot + pos] = (uint16_t)FC_LOC(q);
         a.val[slot + pos] = FAST ? x[q] : a.g[base + FC_LOC(q)];
       }
+      if (dense_too) dense_out(q, p);
+    }
+  };
+  if (!PKT) {                                           // dense only: q, no entries
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) dense_out(q, mag_listed<FAST>(P, x[q]));
+  } else if (tot_e <= (uint32_t)SH::kStageN) {          // block-uniform
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const bool p = mag_listed<FAST>(P, x[q]);
+      const uint32_t pos = prefix_count(__ballot(p)) + goff_of(q);
+      if (p) sh.st[pos] = make_uint2(FC_LOC(q), __float_as_uint(FAST ? x[q] : a.g[base + FC_LOC(q)]));
       dense_out(q, p);
     }
+  } else {
+    direct_entries(true);
   }
   // ---- candidates (key in [t_lo, t_hi]): wave w stages them in its own LDS sub-slot of kCW
   // at a wave-uniform running count: no atomic and no branch per group (a per-group LDS atomic
@@ -891,7 +902,8 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
     atomicAdd(&S->shard_ent[chunk % kShards], tot_e);
     if (tot_c) atomicAdd(&S->shard_cnd[chunk % kShards], tot_c);
   }
-  if (tot_e <= (uint32_t)SH::kStageN) {                 // coalesced 16-B stores of the staged slot
+  if (!PKT && c_ovf) direct_entries(false);            // rare: the resolve reads them
+  if (PKT && tot_e <= (uint32_t)SH::kStageN) {          // coalesced 16-B stores of the staged slot
     for (uint32_t t = 4 * tid; t < tot_e; t += 4 * MagGeo<NW>::kThreads) {
       if (t + 4 <= tot_e) {
         const uint4 p0 = *reinterpret_cast<const uint4*>(&sh.st[t]);
@@ -1031,7 +1043,7 @@ __device__ __forceinline__ void mag_load(const float* g, uint32_t chunk, uint64_
 // workgroups per CU overlap one another's load latency.  (A persistent variant that kept the
 // next item's loads in flight measured 1.3-2.5x SLOWER: hipcc spilled the second register set
 // and loop-carried state)
-template <int NW, typename SH, bool DENSE, bool BIN>
+template <int NW, typename SH, bool DENSE, bool BIN, bool PKT = true>
 __device__ __forceinline__ void compact_mag_item(const CompactArgs& a0, const MagOut& o,
                                                  uint32_t chunk, const MagState& st,
                                                  float (&x)[MagGeo<NW>::kQ], SH& sh) {
@@ -1053,7 +1065,7 @@ __device__ __forceinline__ void compact_mag_item(const CompactArgs& a0, const Ma
   P.cand_all = P.t_hi >= 0x7f800001u;
   P.T_hi = __uint_as_float(P.cand_all ? 0x7f800000u : P.t_hi);
   if (fast) {
-    compact_mag_body<true, SH, NW, DENSE, BIN>(o, P, x, sh, chunk, st.sbin);
+    compact_mag_body<true, SH, NW, DENSE, BIN, PKT>(o, P, x, sh, chunk, st.sbin);
   } else if (none) {                                       // k = 0: nothing listed
     SH::barrier();
     if (tid == 0) {
@@ -1066,7 +1078,7 @@ __device__ __forceinline__ void compact_mag_item(const CompactArgs& a0, const Ma
         o.dense[base + i] = 0.0f;
   } else {                                                 // rare: exact integer predicate
     mag_exact_bits<NW>(P, x, base + (uint32_t)((tid >> 6) * 256 + lane_id()));
-    compact_mag_body<false, SH, NW, DENSE, BIN>(o, P, x, sh, chunk, st.sbin);
+    compact_mag_body<false, SH, NW, DENSE, BIN, PKT>(o, P, x, sh, chunk, st.sbin);
   }
 }
 
@@ -1147,6 +1159,17 @@ union FusedShared {
   MagShared m;
 };
 
+// Candidate binning inside the fused launch (one device-scope atomic per candidate into the
+// candidate histogram) or in k_resolve (rbin) — per variant, see fc_capi.hip
+#ifndef FC_FUSED_BIN_DENSE
+#define FC_FUSED_BIN_DENSE 1
+#endif
+#ifndef FC_FUSED_BIN_PKT
+#define FC_FUSED_BIN_PKT 0
+#endif
+#ifndef FC_DENSE_PKT
+#define FC_DENSE_PKT 0        // 1: the dense path also writes every packet entry (A/B only)
+#endif
 template <bool DENSE>
 __global__ __launch_bounds__(kCBlock, FC_MAG1_WAVES_PER_EU) void k_fused_mag(CompactArgs a0, SamplePlan P,
                                                                               HdrInit HI, uint32_t nsamp) {
@@ -1176,7 +1199,8 @@ __global__ __launch_bounds__(kCBlock, FC_MAG1_WAVES_PER_EU) void k_fused_mag(Com
   __syncthreads();
   FC_TR(25);
   const MagState st = s_st;
-  compact_mag_item<8, MagShared, DENSE, true>(a0, mag_out(a0, 0u), chunk, st, x, u.m);
+  constexpr bool kBin = DENSE ? FC_FUSED_BIN_DENSE != 0 : FC_FUSED_BIN_PKT != 0;
+  compact_mag_item<8, MagShared, DENSE, kBin, !DENSE || FC_DENSE_PKT != 0>(a0, mag_out(a0, 0u), chunk, st, x, u.m);
   FC_TR(26);
 }
 template __global__ void k_fused_mag<false>(CompactArgs, SamplePlan, HdrInit, uint32_t);

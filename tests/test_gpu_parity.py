@@ -203,7 +203,7 @@ def test_top_wave_candidate_overflow(path):
             _check_top_packet(x, k, p, codec.decode(p).cpu().numpy())
     else:
         pkt, q = _dense_top(g, k)
-        _check_top_packet(g, k, pkt, q)
+        _check_dense(g, k, pkt, q)
 
 
 # ---- top straight to the dense q (fc_topk_encode_dense: compaction streams q + fix-up) ----
@@ -215,6 +215,23 @@ def _dense_top(g_np, k):
     return pkt, q
 
 
+def _check_dense(g_np, k, pkt, q):
+    """The dense path's product is q (its packet is scratch, FC_FMT_DENSE): q equals the
+    oracle's and the header's T64 is the oracle's threshold; the scratch packet refuses to
+    decode.  A bracket miss re-encoded the packet exactly (then it is a full packet)."""
+    keys = po.mag_key(g_np)
+    want_idx = po.selected_indices(keys, k)
+    assert q.tobytes() == po.decode_dense(g_np.shape[0], want_idx, g_np[want_idx]).tobytes()
+    h = pkt.header()
+    assert h.status == 0
+    assert np.uint64(h.thresh) == po.threshold(keys, k)
+    if h.format == _L().FC_FMT_DENSE:
+        with pytest.raises(ValueError):
+            _codec().decode(pkt)
+    else:
+        _check_top_packet(g_np, k, pkt, q)
+
+
 @pytest.mark.parametrize("n", [5, 8192, 8193, 100_003, (1 << 20) + 17, 3_000_001])
 @pytest.mark.parametrize("f", [0.1, 0.01, 0.5, 0.999])
 def test_top_dense_sizes(n, f):
@@ -222,7 +239,7 @@ def test_top_dense_sizes(n, f):
     g *= np.float32(10.0) ** np.random.default_rng(n + 1).uniform(-4, 1, n).astype(np.float32)
     k = co.effective_k(co.num_kept(f, n), n)
     pkt, q = _dense_top(g, k)
-    _check_top_packet(g, k, pkt, q)
+    _check_dense(g, k, pkt, q)
 
 
 @pytest.mark.parametrize("kind", sorted(ADVERSARIAL))
@@ -231,7 +248,7 @@ def test_top_dense_adversarial(kind):
     g = ADVERSARIAL[kind](n)
     k = co.effective_k(co.num_kept(f, n), n)
     pkt, q = _dense_top(g, k)
-    _check_top_packet(g, k, pkt, q)
+    _check_dense(g, k, pkt, q)
 
 
 def test_top_dense_golden_and_bracket_miss():
@@ -256,7 +273,7 @@ def test_top_dense_golden_and_bracket_miss():
     g[hidden[: n // 8]] = np.random.default_rng(0).standard_normal(n // 8).astype(np.float32)
     k = n // 10
     pkt, q = _dense_top(g, k)
-    _check_top_packet(g, k, pkt, q)
+    _check_dense(g, k, pkt, q)
 
 
 def test_top_dense_128M_equals_packet_decode():
