@@ -175,6 +175,15 @@ def cpu_matrix(n16=16_777_216, n25=25_557_032):
     g25 = np.random.default_rng(2).standard_normal(n25, dtype=np.float32) * np.float32(1e-2)
     t_top25 = row("top_f0.01_25.5M", {"compression_function": "top", "fraction_coordinate": 0.01}, g25)
     del g25
+    # BASELINE configs[0]: one 4-client round on LeNet-sized gradients (431,080), top f = 0.1
+    # (client_config.json:50), compress per client + FedAvg (aggregation.py:61-63, gar.py:44)
+    gl = [np.random.default_rng(10 + i).standard_normal(431_080, dtype=np.float32) * np.float32(1e-3)
+          for i in range(4)]
+    cfg0 = {"compression_function": "top", "fraction_coordinate": 0.1}
+    _, t0 = _timed(lambda: go.FedAvgOracle({}).aggregate(
+        go.build_dense_G([co.compress(cfg0, x, argsort_kind=None) for x in gl], np.float32)))
+    rows["configs0_4x431080_top0.1_round"] = {"ms": round(1e3 * t0, 1),
+                                              "GBps": round(4 * 4.0 * 431_080 / t0 / 1e9, 4)}
     G = np.stack([g * np.float32(0.5 ** i) for i in range(4)])
     _, t_avg4 = _timed(lambda: go.FedAvgOracle({}).aggregate(G))
     rows["fedavg_4x16M"] = {"ms": round(1e3 * t_avg4, 1), "GBps_of_G": round(G.nbytes / t_avg4 / 1e9, 4)}
