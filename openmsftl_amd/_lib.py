@@ -151,7 +151,12 @@ def load(path: str = LIB_PATH):
         except OSError as e:
             raise FedCodecUnavailable(f"cannot load {path}: {e}") from e
         for name, (res, args) in SIGNATURES.items():
-            fn = getattr(lib, name)
+            try:
+                fn = getattr(lib, name)
+            except AttributeError:
+                if path == LIB_PATH:            # the product library must export every entry
+                    raise
+                continue                        # an older A/B build (tools/ab.py --lib)
             fn.restype = res
             fn.argtypes = args
         if lib.fc_abi_version() != 3:

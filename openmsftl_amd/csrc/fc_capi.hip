@@ -208,13 +208,47 @@ static void launch_compact_mag(const CompactArgs& a, uint32_t m, hipStream_t s) 
   hipLaunchKernelGGL(k_compact_mag1, dim3(a.nchunks, m), dim3(kCBlock), 0, s, a);
 }
 
-static int launch_compact_key(int key_mode, const CompactArgs& a, hipStream_t s) {
+static int launch_compact_key(int key_mode, const CompactArgs& a, hipStream_t s, uint32_t m = 1) {
   TimedLaunch t(FC_TIME_COMPACT, s);
   if (key_mode == FC_KEY_PHILOX)
-    hipLaunchKernelGGL((k_compact<kKeyPhilox, kPredKey, FC_FMT_IDXVAL>), dim3(a.nchunks), dim3(kCBlock), 0, s, a);
+    hipLaunchKernelGGL((k_compact_pred<kSrcPhiloxKey, FC_FMT_IDXVAL>), dim3(a.nchunks, m), dim3(kCBlock), 0, s, a);
   else
-    launch_compact_mag(a, 1, s);
+    launch_compact_mag(a, m, s);
   FC_LAUNCHED("k_compact");
+  return FC_OK;
+}
+
+// Native rand-k: the keys (Philox word >> 1) are uniform on [0, 2^31), so #(key > t) is
+// Binomial(n, (2^31 - 1 - t) / 2^31) and the bracket around the k-th key needs no sample:
+// t_hi puts k - 8 sigma - 16 keys above it on average, t_lo k + 8 sigma + 16 at or above it
+// (a miss is ~1e-15 likely and only costs the exact re-encode).  ~16 sigma candidates.
+static void philox_bracket(uint64_t n, uint64_t k, uint32_t* t_lo, uint32_t* t_hi, uint32_t* sbin) {
+  const double N = (double)n, K = (double)k, R = 2147483648.0;
+  const double M = 8.0 * sqrt(K * (1.0 - K / N)) + 16.0;
+  auto key_for = [&](double above) { return R - 1.0 - above * R / N; };   // E #(key > t) = above
+  double hi = K - M <= 0.0 ? R - 1.0 : ceil(key_for(K - M));
+  double lo = K + M >= N ? 0.0 : floor(key_for(K + M));
+  hi = std::min(std::max(hi, 0.0), R - 1.0);
+  lo = std::min(std::max(lo, 0.0), hi);
+  *t_hi = (uint32_t)hi;
+  *t_lo = (uint32_t)lo;
+  const uint64_t span = (uint64_t)*t_hi - *t_lo;
+  uint32_t sb = 0;
+  while ((span >> sb) >= (uint64_t)kHistBins) ++sb;
+  *sbin = sb;
+}
+
+// k_setup_bracket for one client (jobs == nullptr) or a batch (grid = clients)
+static int launch_setup(uint64_t n, uint64_t k, const WsPtrs& W, fc_packet_hdr* hdr,
+                        const HdrInit& hi, const fc_encode_job* jobs, uint64_t stride,
+                        uint32_t m, hipStream_t s) {
+  SetupArgs a;
+  memset(&a, 0, sizeof a);
+  a.W = W; a.hdr = hdr; a.HI = hi; a.jobs = jobs; a.ws_stride = stride; a.ib = hi.ib;
+  philox_bracket(n, k, &a.t_lo, &a.t_hi, &a.sbin);
+  TimedLaunch t(FC_TIME_SAMPLE, s);
+  hipLaunchKernelGGL(k_setup_bracket, dim3(m), dim3(64), 0, s, a);
+  FC_LAUNCHED("k_setup_bracket");
   return FC_OK;
 }
 
@@ -362,11 +396,14 @@ int fc_topk_encode(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_
     ra.rbin = FC_FUSED_BIN_PKT ? 0u : 1u;
     return launch_resolve(ra, s);
   }
-  rc = launch_sample(key_mode, dim3(sgrid), g, P, seed, offset, ca.W, ca.ib, hdr, hi, nullptr, 0ull, s);
+  if (key_mode == FC_KEY_PHILOX)      // uniform keys: the analytical bracket, no sample
+    rc = launch_setup(n, k, ca.W, hdr, hi, nullptr, 0ull, 1, s);
+  else
+    rc = launch_sample(key_mode, dim3(sgrid), g, P, seed, offset, ca.W, ca.ib, hdr, hi, nullptr, 0ull, s);
   if (rc) return rc;
   rc = launch_compact_key(key_mode, ca, s);
   if (rc) return rc;
-  ra.rbin = 1;                       // k_compact / k_compact_mag1 leave the binning to k_resolve
+  ra.rbin = 1;                       // the unfused compactions leave the binning to k_resolve
   return launch_resolve(ra, s);
 }
 
@@ -452,18 +489,15 @@ int fc_topk_encode_batch_part(const fc_encode_job* jobs, int m, uint64_t n, uint
   const SamplePlan P = make_plan(n, k);
   const dim3 sgrid((P.nseg + kSampleSegs - 1) / kSampleSegs, (uint32_t)m);
   if (part & FC_PART_SAMPLE) {
-    int rc = launch_sample(key_mode, sgrid, nullptr, P, 0ull, 0ull, ca.W, ib, nullptr, hi, jobs, stride, s);
+    int rc = key_mode == FC_KEY_PHILOX
+                 ? launch_setup(n, k, ca.W, nullptr, hi, jobs, stride, (uint32_t)m, s)
+                 : launch_sample(key_mode, sgrid, nullptr, P, 0ull, 0ull, ca.W, ib, nullptr, hi, jobs, stride, s);
     if (rc) return rc;
   }
   if (!(part & FC_PART_FINISH)) return FC_OK;
   {
-    TimedLaunch t(FC_TIME_COMPACT, s);
-    const dim3 grid(ca.nchunks, (uint32_t)m);
-    if (key_mode == FC_KEY_PHILOX)
-      hipLaunchKernelGGL((k_compact<kKeyPhilox, kPredKey, FC_FMT_IDXVAL>), grid, dim3(kCBlock), 0, s, ca);
-    else
-      launch_compact_mag(ca, (uint32_t)m, s);
-    FC_LAUNCHED("k_compact(batch)");
+    int rc = launch_compact_key(key_mode, ca, s, (uint32_t)m);
+    if (rc) return rc;
   }
   {
     TimedLaunch t(FC_TIME_ENGINE, s);
@@ -512,11 +546,11 @@ int fc_mask_encode(const float* g, uint64_t n, int codec, const uint32_t* mask_b
   const dim3 grid(a.nchunks), blk(kCBlock);
   TimedLaunch t(FC_TIME_COMPACT, s);
   if (mask_bits) {
-    if (format == FC_FMT_BITMAP) hipLaunchKernelGGL((k_compact<kKeyMag, kPredMask, FC_FMT_BITMAP>), grid, blk, 0, s, a);
-    else hipLaunchKernelGGL((k_compact<kKeyMag, kPredMask, FC_FMT_IDXVAL>), grid, blk, 0, s, a);
+    if (format == FC_FMT_BITMAP) hipLaunchKernelGGL((k_compact_pred<kSrcMaskBits, FC_FMT_BITMAP>), grid, blk, 0, s, a);
+    else hipLaunchKernelGGL((k_compact_pred<kSrcMaskBits, FC_FMT_IDXVAL>), grid, blk, 0, s, a);
   } else {
-    if (format == FC_FMT_BITMAP) hipLaunchKernelGGL((k_compact<kKeyMag, kPredBern, FC_FMT_BITMAP>), grid, blk, 0, s, a);
-    else hipLaunchKernelGGL((k_compact<kKeyMag, kPredBern, FC_FMT_IDXVAL>), grid, blk, 0, s, a);
+    if (format == FC_FMT_BITMAP) hipLaunchKernelGGL((k_compact_pred<kSrcBern, FC_FMT_BITMAP>), grid, blk, 0, s, a);
+    else hipLaunchKernelGGL((k_compact_pred<kSrcBern, FC_FMT_IDXVAL>), grid, blk, 0, s, a);
   }
   FC_LAUNCHED("k_compact(mask)");
   return FC_OK;

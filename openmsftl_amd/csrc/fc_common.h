@@ -67,15 +67,25 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1
   }
   return c;
 }
-// the four words for elements 4b .. 4b+3
+// counter block b: (lo32 b, hi32 b, lo32 offset, hi32 offset), key = seed
 __device__ __forceinline__ uint4 philox_block(uint64_t b, uint64_t seed, uint64_t offset) {
   return philox4x32_10(make_uint4((uint32_t)b, (uint32_t)(b >> 32), (uint32_t)offset,
                                   (uint32_t)(offset >> 32)),
                        (uint32_t)seed, (uint32_t)(seed >> 32));
 }
+// The codec's element -> word map (native rand-k keys, Bernoulli dropout masks):
+//     element i  ->  block ((i >> 8) << 6) | (i & 63),  word (i >> 6) & 3
+// The four words of a block go to elements 64 apart, so in the ballot layout (element
+// seg*256 + j*64 + lane) lane L computes ONE block per 256-element segment and holds the
+// words of its four groups j (oracle/philox.py element_words).  (QSGD keeps its own linear
+// map, block i >> 2, for 8 consecutive elements per thread.)
+__device__ __forceinline__ uint4 philox_seg(uint64_t seg, uint32_t lane, uint64_t seed,
+                                            uint64_t offset) {
+  return philox_block((seg << 6) | lane, seed, offset);
+}
 __device__ __forceinline__ uint32_t philox_word(uint64_t i, uint64_t seed, uint64_t offset) {
-  const uint4 r = philox_block(i >> 2, seed, offset);
-  const uint32_t s = (uint32_t)(i & 3);
+  const uint4 r = philox_seg(i >> 8, (uint32_t)(i & 63), seed, offset);
+  const uint32_t s = (uint32_t)(i >> 6) & 3u;
   return s == 0 ? r.x : s == 1 ? r.y : s == 2 ? r.z : r.w;
 }
 

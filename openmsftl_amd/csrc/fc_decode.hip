@@ -718,7 +718,10 @@ __global__ __launch_bounds__(kQBlock, 4) void k_fold_q(DecodeArgs a) {
     const uint32_t codec = h->codec, key_mode = h->key_mode;
     const float dz = (codec == FC_CODEC_DROPOUT_UNBIASED && h->p == 0.0) ? __uint_as_float(0x7fc00000u) : 0.0f;
     const bool poison = __fmul_rn(dz, v.weight) != __fmul_rn(dz, v.weight);
-    const bool generic = codec == FC_CODEC_DROPOUT_UNBIASED || (key_mode == FC_KEY_PHILOX && d.thresh != 0);
+    // the fast body's float form of comp >= T64 needs T64's key below +inf bits (k = 0's
+    // kSelectNothing and an inf / NaN k-th element take the per-entry rules)
+    const bool generic = codec == FC_CODEC_DROPOUT_UNBIASED || (key_mode == FC_KEY_PHILOX && d.thresh != 0) ||
+                         (d.thresh >> (h->index_bits & 0xffu)) >= 0x7f800000ull;
     d.flags = (h->index_bits & 0xffu) | ((codec & 0xffu) << 8) | ((key_mode & 0xffu) << 16) |
               ((uint32_t)poison << 24) | (v.qoff ? 0u : kQNoQoff);
     s_meta[tid] = d;
@@ -746,7 +749,10 @@ __global__ __launch_bounds__(kQBlock, 4) void k_fold_q(DecodeArgs a) {
     const uint32_t en = q == 3 ? (uint32_t)(v >> 48) : (uint32_t)(v >> (16 * q)) & 0xffffu;
     return en - st;
   };
-  const bool dense_q = __any(qcount(qo0) > (uint32_t)(kQTail * 64) || qcount(qo1) > (uint32_t)(kQTail * 64));
+  // (the last chunk too: the fast body reads up to 255 entries past a quarter's end without a
+  // clamp, which stays inside the packet only while a next chunk's slot follows)
+  const bool dense_q = __any(qcount(qo0) > (uint32_t)(kQTail * 64) || qcount(qo1) > (uint32_t)(kQTail * 64)) ||
+                       c + 1u == gridDim.x;
   auto range = [&](uint32_t m, uint32_t& st, uint32_t& en) {   // uniform
     const uint64_t src = m < 64 ? qo0 : qo1;
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)src, (int)(m & 63));
@@ -798,26 +804,32 @@ __global__ __launch_bounds__(kQBlock, 4) void k_fold_q(DecodeArgs a) {
     }
   } else {
     // ---- fast body: top-k / mask-selected packets; two register slots of kQGroup items, the
-    // loads of one group in flight while the other is folded (every wait a partial vmcnt) ----
+    // loads of one group in flight while the other is folded (every wait a partial vmcnt).
+    // Per entry: loc = lc & 2047 (lc - q * 2048 for an entry of this quarter), one count
+    // compare and comp >= T64 in float form:
+    //     comp >= T64  <=>  !(|v| <= Tf)  ||  (|v| == Tf && lc >= Ti - chunk base)
+    // (Tf = T64's key as a float; NaN is unordered -> kept, its key is above every finite T).
+    // The entry loads are not clamped: lanes past the quarter's end read the next entries of
+    // the packet (the last chunk takes the slow body), are never written, and their tile read
+    // is masked into the quarter.  (Round 2's form — clamped loads, 64-bit comps and a branch
+    // per read — spent 34 VALU lane-ops per entry; the fold was VALU-bound.)
     uint32_t ids_[2][kQGroup][kQR];
     float vs_[2][kQGroup][kQR];
-    uint32_t st_[2][kQGroup], en_[2][kQGroup];
+    uint32_t qn_[2][kQGroup];                                   // the item's entries (uniform)
     auto issue = [&](int sl, uint32_t m0) {
 #pragma unroll
       for (int d = 0; d < kQGroup; ++d) {
         const uint32_t m = min(m0 + (uint32_t)d, M - 1);          // past the end: re-load (ignored)
         uint32_t st, en;
         range(m, st, en);
-        st_[sl][d] = st; en_[sl][d] = en;
+        qn_[sl][d] = en - st;
         const QMeta& pm = s_meta[m];
-        gf32* val = (gf32*)uni_ptr(pm.val) + base;
-        gu16* idx = (gu16*)uni_ptr(pm.idx) + base;
-        const uint32_t last = en > st ? en - 1 : st;
+        gf32* val = (gf32*)uni_ptr(pm.val) + base + st;
+        gu16* idx = (gu16*)uni_ptr(pm.idx) + base + st;
 #pragma unroll
         for (int r = 0; r < kQR; ++r) {
-          const uint32_t e = min(st + (uint32_t)(lane + r * 64), last);
-          vs_[sl][d][r] = val[e];
-          ids_[sl][d][r] = idx[e];
+          vs_[sl][d][r] = val[lane + r * 64];
+          ids_[sl][d][r] = idx[lane + r * 64];
         }
       }
     };
@@ -830,13 +842,12 @@ __global__ __launch_bounds__(kQBlock, 4) void k_fold_q(DecodeArgs a) {
         const float w = __uint_as_float(uni32(__float_as_uint(pm.w)));
         const uint64_t thresh = uni64(pm.thresh);
         const uint32_t ib = uni32(pm.flags) & 0xffu;
-        const uint32_t st = st_[sl][d], en = en_[sl][d];
-        // slack filter comp >= T64 (T64 = 0 keeps every entry: comp >= 0).  Measured slower:
-        // a per-item float threshold |v| !< Tf behind a uniform exact/fast branch (+4 %),
-        // skipping the rounds past the item's count (+27 %) — control flow inside the unrolled
-        // group costs more than the VALU it saves — and one no-return ds_add_f32 per entry
-        // instead of the read + write (bit-exact, but 3.7x slower).
+        const float Tf = __uint_as_float((uint32_t)(thresh >> ib));
+        const uint32_t Ti = (uint32_t)(thresh & ((1ull << ib) - 1ull));
         const uint32_t b32 = (uint32_t)base;
+        const uint32_t Tr = Ti <= b32 ? 0u : min(Ti - b32, (uint32_t)kChunk);   // tie cut in the chunk
+        const uint32_t qn = qn_[sl][d];
+        const int lim = (int)qn - lane;                           // entries left for this lane
         uint32_t loc[kQR];
         bool ok[kQR];
         float tv[kQR];
@@ -844,22 +855,25 @@ __global__ __launch_bounds__(kQBlock, 4) void k_fold_q(DecodeArgs a) {
         for (int r = 0; r < kQR; ++r) {                           // all tile reads, then writes
           const uint32_t lc = ids_[sl][d][r];                     // chunk-local
           const float v = vs_[sl][d][r];
-          loc[r] = lc - (uint32_t)(q * kQuarter);
-          ok[r] = st + (uint32_t)(lane + r * 64) < en && loc[r] < (uint32_t)kQuarter &&
-                  comp_of(mag_key(v), b32 + lc, ib) >= thresh;
-          tv[r] = ok[r] ? qt[loc[r]] : 0.f;
+          const float av = __builtin_fabsf(v);
+          loc[r] = lc & (uint32_t)(kQuarter - 1);
+          ok[r] = (lim > r * 64) & (!(av <= Tf) | ((av == Tf) & (lc >= Tr)));
+          tv[r] = qt[loc[r]];
         }
 #pragma unroll
         for (int r = 0; r < kQR; ++r)
           if (ok[r]) qt[loc[r]] = __fadd_rn(tv[r], __fmul_rn(vs_[sl][d][r], w));
-        if (kQTail > kQR && en - st > (uint32_t)(kQR * 64)) {      // rare, uniform: the rest
+        if (kQTail > kQR && qn > (uint32_t)(kQR * 64)) {          // rare, uniform: the rest
+          uint32_t st, en;
+          range(m, st, en);
           gf32* val = (gf32*)uni_ptr(pm.val) + base;
           gu16* idx = (gu16*)uni_ptr(pm.idx) + base;
           for (uint32_t e = st + (uint32_t)(kQR * 64) + lane; e < en; e += 64) {
             const uint32_t lc = idx[e];
             const float v = val[e];
-            const uint32_t l2 = lc - (uint32_t)(q * kQuarter);
-            if (l2 < (uint32_t)kQuarter && comp_of(mag_key(v), b32 + lc, ib) >= thresh)
+            const float av = __builtin_fabsf(v);
+            const uint32_t l2 = lc & (uint32_t)(kQuarter - 1);
+            if (!(av <= Tf) | ((av == Tf) & (lc >= Tr)))
               qt[l2] = __fadd_rn(qt[l2], __fmul_rn(v, w));
           }
         }

@@ -21,7 +21,7 @@
 //
 // Anything unusual (bracket missed, candidate list overflow, > 4096 survivors) sets
 // FC_STATUS_RETRY_EXACT; fc_topk_encode_exact then runs k_engine (12-bit radix select over
-// g, <= 6 passes) followed by k_compact with L64 = T64 (no slack).
+// g, <= 6 passes) followed by the compaction with L64 = T64 (no slack).
 //
 // Selection rule: comp = key << IB | idx is unique per element; the k
 // largest comps are kept <=> argsort(|g|, stable)[::-1][:k] (highest index first in a tie),
@@ -37,8 +37,8 @@ template <int KM>
 __device__ __forceinline__ uint4 keys4(const float4& x, uint64_t e, uint64_t seed,
                                        uint64_t off) {
   if (KM == kKeyMag) return make_uint4(mag_key(x.x), mag_key(x.y), mag_key(x.z), mag_key(x.w));
-  const uint4 r = philox_block(e >> 2, seed, off);    // e is a multiple of 4
-  return make_uint4(r.x >> 1, r.y >> 1, r.z >> 1, r.w >> 1);
+  return make_uint4(philox_word(e, seed, off) >> 1, philox_word(e + 1, seed, off) >> 1,
+                    philox_word(e + 2, seed, off) >> 1, philox_word(e + 3, seed, off) >> 1);
 }
 template <int KM>
 __device__ __forceinline__ uint32_t key1(float x, uint64_t i, uint64_t seed, uint64_t off) {
@@ -384,29 +384,22 @@ __global__ __launch_bounds__(kBlock) void k_sample1(const float* __restrict__ g,
 
 
 // --------------------------------------------------------------------------------------
-// k_compact: one independent 512-thread workgroup per 8192-element chunk (slotted packet,
-// no global scan).  Element layout: e = i*2048 + w*256 + lane*4 + j (i < 4, w < 8, j < 4):
-// each wave instruction moves 1 KiB contiguous and (i, w, lane, j) order is ascending index
-// order, so ballot + mbcnt + a 32-slot LDS scan give ordered offsets inside the chunk's slot.
-// Listed entries are staged in LDS and leave as coalesced 16-B stores; candidates go to the
-// chunk's candidate slot (k_resolve bins them).
+// Compaction (k_compact_mag1 here, k_compact_pred in fc_pred.hip): one independent 512-thread
+// workgroup per 8192-element chunk (slotted packet, no global scan).  Listed entries are
+// staged in LDS and leave as coalesced 16-B stores; candidates go to the chunk's candidate
+// slot (k_resolve bins them).
 // --------------------------------------------------------------------------------------
-enum Pred : int { kPredKey = 0, kPredMask = 1, kPredBern = 2 };
-
 constexpr int kCBlock = 512;
 constexpr int kCWaves = kCBlock / 64;            // 8
-constexpr int kCVec = kChunk / (kCBlock * 4);    // 4 float4 per thread
-constexpr int kCSlots = kCVec * kCWaves;         // 32
 constexpr int kStage = 2048;                     // LDS-staged entries per chunk
-static_assert(kCSlots == 32, "slot scan assumes 32 slots");
 
 struct CompactArgs {
   const float* g;
   uint64_t n;
   uint32_t ib, nchunks;
   uint64_t seed, offset;
-  const uint32_t* mask;     // kPredMask
-  uint64_t bern_thr;        // kPredBern: keep iff word < thr
+  const uint32_t* mask;     // kSrcMaskBits (fc_pred.hip): host keep mask
+  uint64_t bern_thr;        // kSrcBern: keep iff Philox word < thr
   uint32_t nonfinite_keep;  // dropout: dropped inf/NaN are listed as NaN (g * 0 == NaN)
   uint32_t write_hdr;       // mask pipelines (no earlier kernel) write the static header
   uint16_t* idx;            // chunk-local indices (ABI 3)
@@ -431,234 +424,6 @@ __device__ __forceinline__ void apply_job(Args& a) {
   if constexpr (std::is_same<Args, CompactArgs>::value) a.qoff = J.qoff;
   a.seed = J.seed; a.offset = J.offset;
   a.W = ws_shift(a.W, (uint64_t)blockIdx.y * a.ws_stride);
-}
-
-// Stage the listed elements of one float4 (bits 0..3 of `bb`) at LDS positions pos, pos+1..
-// as packed {chunk-local index, value bits}.  LDS store cost is per wave instruction, not per
-// active lane: instead of one store per element, run only as many rounds as the busiest lane
-// of the wave has listed elements (~2 at f = 0.1), one b64 store per round.  Lanes with
-// nothing left write their private dummy slot kStage + lane (branchless, conflict-free).
-template <int PRED>
-__device__ __forceinline__ void stage_f4(uint2* st, float4 v4, uint32_t bb, uint32_t nanb,
-                                         uint32_t pos, uint32_t l0, int lane) {
-  bb &= 0xfu;
-  while (__any(bb != 0u)) {
-    const bool sel = bb != 0u;
-    const uint32_t j = (uint32_t)__builtin_ctz(bb | 0x10u);
-    float v = j == 0 ? v4.x : j == 1 ? v4.y : j == 2 ? v4.z : v4.w;
-    if (PRED != kPredKey) v = ((nanb >> j) & 1u) ? __uint_as_float(0x7fc00000u) : v;
-    st[sel ? pos : (uint32_t)kStage + lane] = make_uint2(l0 + j, __float_as_uint(v));
-    pos += sel;
-    bb &= bb - 1u;
-  }
-}
-
-#ifndef FC_COMPACT_WAVES_PER_EU
-#define FC_COMPACT_WAVES_PER_EU 6
-#endif
-template <int KM, int PRED, int FMT>
-__global__ __launch_bounds__(kCBlock, FC_COMPACT_WAVES_PER_EU) void k_compact(CompactArgs a0) {
-  CompactArgs a = a0;
-  if (a.jobs) { a.g = a.jobs[blockIdx.y].g; apply_job(a); }
-  __shared__ uint32_t s_ent[kCSlots], s_cnd[kCSlots], s_tot[2];
-  // staging: one packed {chunk-local index, value bits} per listed element; lanes with
-  // nothing left to write in a round store to their own dummy slot kStage + lane (one shared
-  // dummy made every store a ~58-way LDS bank conflict — measured 65 us of a 165 us launch)
-  __shared__ __attribute__((aligned(16))) uint2 st[kStage + 64];
-  const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
-  TopkState* S = a.W.st;
-  const uint32_t chunk = blockIdx.x;
-  const uint32_t base = chunk * (uint32_t)kChunk;          // n < 2^32
-  const uint32_t n32 = (uint32_t)a.n;
-  if (a.write_hdr && chunk == 0 && tid == 0) write_hdr_static(a.hdr, a.HI);  // sole writer
-
-  // g first: all four loads in flight before anything waits (state loads queue behind them)
-  float4 x[kCVec];
-  if ((uint64_t)base + kChunk <= a.n) {           // block-uniform: whole chunk in range
-#pragma unroll
-    for (int i = 0; i < kCVec; ++i)
-      x[i] = load4_full(a.g + base + (uint32_t)(i * 2048 + w * 256 + lane * 4));
-  } else {
-#pragma unroll
-    for (int i = 0; i < kCVec; ++i)
-      x[i] = load4(a.g, (uint64_t)base + (uint32_t)(i * 2048 + w * 256 + lane * 4), a.n);
-  }
-
-  uint32_t Lk = 0;   // key part of L64; 0xffffffff (above every key) selects nothing
-  uint32_t Li = 0, t_lo = 0, t_hi = 0xffffffffu, cand_on = 0;
-  if (PRED == kPredKey) {
-    const uint64_t L64 = S->L64;
-    const bool none = L64 == kSelectNothing;
-    Lk = none ? 0xffffffffu : (uint32_t)(L64 >> a.ib);
-    Li = none ? 0xffffffffu : (uint32_t)(L64 & ((1ull << a.ib) - 1));
-    t_lo = S->t_lo; t_hi = S->t_hi; cand_on = S->cand_on;
-  }
-
-  // ---- predicates (branchless): bit (i*4 + j) -------------------------------------------
-  uint32_t pbits = 0, cbits = 0;   // listed / candidate (or NaN stand-in for mask codecs)
-#pragma unroll
-  for (int i = 0; i < kCVec; ++i) {
-    const uint32_t e0 = base + (uint32_t)(i * 2048 + w * 256 + lane * 4);
-    uint4 kk = make_uint4(0, 0, 0, 0);
-    if (PRED == kPredKey) kk = keys4<KM>(x[i], e0, a.seed, a.offset);
-    if (PRED == kPredBern) kk = philox_block(e0 >> 2, a.seed, a.offset);
-    uint32_t mword = 0;
-    if (PRED == kPredMask && e0 < n32) mword = a.mask[e0 >> 5] >> (e0 & 31);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t e = e0 + j;
-      const bool valid = e < n32;
-      bool p, c;
-      if (PRED == kPredKey) {
-        const uint32_t key = u4get(kk, j);
-        p = valid & ((key > Lk) | ((key == Lk) & (e >= Li)));          // branchless
-        c = valid & (cand_on != 0) & (key >= t_lo) & (key <= t_hi);
-      } else {
-        const bool keep = PRED == kPredMask ? ((mword >> j) & 1u) != 0
-                                            : (uint64_t)u4get(kk, j) < a.bern_thr;
-        const uint32_t ab = __float_as_uint(f4get(x[i], j)) & 0x7fffffffu;
-        c = a.nonfinite_keep && !keep && ab >= 0x7f800000u;    // g*0 = NaN stand-in
-        p = valid && (keep || c);
-        c = c && valid;
-      }
-      pbits |= (uint32_t)p << (i * 4 + j);
-      cbits |= (uint32_t)c << (i * 4 + j);
-    }
-  }
-
-  // ---- ordered offsets: per-i lane counts packed 2 x 16 bit, one DPP scan per pair ----------
-  const uint32_t c01 = __popc(pbits & 0xfu) | (__popc((pbits >> 4) & 0xfu) << 16);
-  const uint32_t c23 = __popc((pbits >> 8) & 0xfu) | (__popc((pbits >> 12) & 0xfu) << 16);
-  const uint32_t i01 = wave_incl_scan(c01), i23 = wave_incl_scan(c23);
-  const uint32_t x01 = i01 - c01, x23 = i23 - c23;         // exclusive (no field borrow)
-  if (lane == 63) {
-    s_ent[0 * kCWaves + w] = i01 & 0xffffu; s_ent[1 * kCWaves + w] = i01 >> 16;
-    s_ent[2 * kCWaves + w] = i23 & 0xffffu; s_ent[3 * kCWaves + w] = i23 >> 16;
-  }
-  const bool wave_cand = PRED == kPredKey && __any(cbits != 0);
-  uint32_t xc01 = 0, xc23 = 0;
-  if (PRED == kPredKey) {
-    if (wave_cand) {
-      const uint32_t d01 = __popc(cbits & 0xfu) | (__popc((cbits >> 4) & 0xfu) << 16);
-      const uint32_t d23 = __popc((cbits >> 8) & 0xfu) | (__popc((cbits >> 12) & 0xfu) << 16);
-      const uint32_t j01 = wave_incl_scan(d01), j23 = wave_incl_scan(d23);
-      xc01 = j01 - d01; xc23 = j23 - d23;
-      if (lane == 63) {
-        s_cnd[0 * kCWaves + w] = j01 & 0xffffu; s_cnd[1 * kCWaves + w] = j01 >> 16;
-        s_cnd[2 * kCWaves + w] = j23 & 0xffffu; s_cnd[3 * kCWaves + w] = j23 >> 16;
-      }
-    } else if (lane == 0) {
-      s_cnd[0 * kCWaves + w] = 0; s_cnd[1 * kCWaves + w] = 0;
-      s_cnd[2 * kCWaves + w] = 0; s_cnd[3 * kCWaves + w] = 0;
-    }
-  }
-  if (FMT == FC_FMT_BITMAP) {   // bitmap words (natural bit order) from 4 ballots per i
-#pragma unroll
-    for (int i = 0; i < kCVec; ++i) {
-      const uint64_t m0 = __ballot((pbits >> (i * 4 + 0)) & 1u);
-      const uint64_t m1 = __ballot((pbits >> (i * 4 + 1)) & 1u);
-      const uint64_t m2 = __ballot((pbits >> (i * 4 + 2)) & 1u);
-      const uint64_t m3 = __ballot((pbits >> (i * 4 + 3)) & 1u);
-      if (lane < 8) {
-        const int sh = lane * 8;
-        const uint32_t word = spread4((uint32_t)(m0 >> sh)) | (spread4((uint32_t)(m1 >> sh)) << 1) |
-                              (spread4((uint32_t)(m2 >> sh)) << 2) | (spread4((uint32_t)(m3 >> sh)) << 3);
-        a.bitmap[(base + (uint32_t)(i * 2048 + w * 256)) / 32 + lane] = word;
-      }
-    }
-  }
-  __syncthreads();
-  if (w == 0) {   // exclusive scan of the 32 (i, w) slots (lanes 0..31) for both counts
-    const uint32_t ve = lane < kCSlots ? s_ent[lane] : 0u, vc = lane < kCSlots ? s_cnd[lane] : 0u;
-    const uint32_t ie = wave_incl_scan(ve);
-    const uint32_t ic = PRED == kPredKey ? wave_incl_scan(vc) : 0u;
-    if (lane < kCSlots) { s_ent[lane] = ie - ve; if (PRED == kPredKey) s_cnd[lane] = ic - vc; }
-    // quarter q of the chunk = slots (q, w): its entries start where slot (q, 0) does
-    const uint32_t q1 = (uint32_t)__builtin_amdgcn_readlane((int)(ie - ve), 1 * kCWaves);
-    const uint32_t q2 = (uint32_t)__builtin_amdgcn_readlane((int)(ie - ve), 2 * kCWaves);
-    const uint32_t q3 = (uint32_t)__builtin_amdgcn_readlane((int)(ie - ve), 3 * kCWaves);
-    if (lane == kCSlots - 1) {
-      s_tot[0] = ie; s_tot[1] = ic;
-      a.cnt[chunk] = ie;
-      if (FMT == FC_FMT_IDXVAL && a.qoff)
-        a.qoff[chunk] = q1 | ((uint64_t)q2 << 16) | ((uint64_t)q3 << 32) | ((uint64_t)ie << 48);
-      if (PRED == kPredKey) {
-        a.W.ccnt[chunk] = ic;
-        atomicAdd(&S->shard_ent[chunk % kShards], ie);
-        if (ic) atomicAdd(&S->shard_cnd[chunk % kShards], ic);
-      }
-    }
-  }
-  __syncthreads();
-
-  const uint32_t tot_e = s_tot[0];
-  const uint64_t slot = base;                     // entries slot of this chunk
-  if (tot_e <= (uint32_t)kStage) {                // block-uniform: stage in LDS
-    // LDS store cost is per wave instruction, not per active lane: instead of one store per
-    // element (32 per thread, ~1 GB of LDS traffic per 128M launch) each float4 runs only as
-    // many rounds as its busiest lane has listed elements (~2 at f = 0.1), one b64 per round.
-    stage_f4<PRED>(st, x[0], pbits, cbits, s_ent[0 * kCWaves + w] + (x01 & 0xffffu), 0 * 2048 + w * 256 + lane * 4, lane);
-    stage_f4<PRED>(st, x[1], pbits >> 4, cbits >> 4, s_ent[1 * kCWaves + w] + (x01 >> 16), 1 * 2048 + w * 256 + lane * 4, lane);
-    stage_f4<PRED>(st, x[2], pbits >> 8, cbits >> 8, s_ent[2 * kCWaves + w] + (x23 & 0xffffu), 2 * 2048 + w * 256 + lane * 4, lane);
-    stage_f4<PRED>(st, x[3], pbits >> 12, cbits >> 12, s_ent[3 * kCWaves + w] + (x23 >> 16), 3 * 2048 + w * 256 + lane * 4, lane);
-  } else {                                        // dense chunk: direct (predicated) stores
-#pragma unroll
-    for (int i = 0; i < kCVec; ++i) {
-      const uint32_t e0 = base + (uint32_t)(i * 2048 + w * 256 + lane * 4);
-      const uint32_t xi = (i & 1) ? ((i < 2 ? x01 : x23) >> 16) : ((i < 2 ? x01 : x23) & 0xffffu);
-      uint32_t pos = s_ent[i * kCWaves + w] + xi;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if ((pbits >> (i * 4 + j)) & 1u) {
-          float v = f4get(x[i], j);
-          if (PRED != kPredKey && ((cbits >> (i * 4 + j)) & 1u)) v = __uint_as_float(0x7fc00000u);
-          if (FMT == FC_FMT_IDXVAL) a.idx[slot + pos] = (uint16_t)(e0 + j - base);
-          a.val[slot + pos] = v;
-          ++pos;
-        }
-      }
-    }
-  }
-  if (wave_cand) {                                // candidates: rare, predicated
-    const uint64_t cslot = (uint64_t)chunk * kCandSlot;
-#pragma unroll
-    for (int i = 0; i < kCVec; ++i) {
-      if (!((cbits >> (i * 4)) & 0xfu)) continue;
-      const uint32_t e0 = base + (uint32_t)(i * 2048 + w * 256 + lane * 4);
-      const uint32_t xi = (i & 1) ? ((i < 2 ? xc01 : xc23) >> 16) : ((i < 2 ? xc01 : xc23) & 0xffffu);
-      uint32_t cpos = s_cnd[i * kCWaves + w] + xi;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if ((cbits >> (i * 4 + j)) & 1u) {
-          // recompute (2 ops) rather than keep 16 keys + indices live across the barriers
-          uint32_t e = e0 + j;
-          float xv = f4get(x[i], j);
-          asm volatile("" : "+v"(xv), "+v"(e));
-          const uint32_t key = key1<KM>(xv, e, a.seed, a.offset);
-          if (cpos < (uint32_t)kCandSlot) a.W.cand[cslot + cpos] = comp_of(key, e, a.ib);
-          ++cpos;
-        }
-      }
-    }
-  }
-  __syncthreads();
-  if (tot_e <= (uint32_t)kStage) {                // coalesced 16-B stores of the staged slot
-    for (uint32_t t = 4 * tid; t < tot_e; t += 4 * kCBlock) {
-      if (t + 4 <= tot_e) {
-        const uint4 p0 = *reinterpret_cast<const uint4*>(&st[t]);
-        const uint4 p1 = *reinterpret_cast<const uint4*>(&st[t + 2]);
-        if (FMT == FC_FMT_IDXVAL)      // 4 chunk-local u16 indices: one 8-B store
-          *reinterpret_cast<uint2*>(a.idx + slot + t) =
-              make_uint2(p0.x | (p0.z << 16), p1.x | (p1.z << 16));
-        *reinterpret_cast<uint4*>(a.val + slot + t) = make_uint4(p0.y, p0.w, p1.y, p1.w);
-      } else {
-        for (uint32_t u = t; u < tot_e; ++u) {
-          if (FMT == FC_FMT_IDXVAL) a.idx[slot + u] = (uint16_t)st[u].x;
-          a.val[slot + u] = __uint_as_float(st[u].y);
-        }
-      }
-    }
-  }
 }
 
 // --------------------------------------------------------------------------------------
@@ -1531,7 +1296,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve(ResolveArgs a0) {
 
 // --------------------------------------------------------------------------------------
 // k_engine: exact pipeline — one 12-bit radix (or final LDS-sort) pass of the selection of
-// the k-th largest comp over g itself.  Runs BEFORE k_compact (which then lists exactly
+// the k-th largest comp over g itself.  Runs BEFORE the compaction (which then lists exactly
 // comp >= T64).  Used for trivial k and whenever the sampled bracket reports RETRY.
 // --------------------------------------------------------------------------------------
 struct EngineArgs {
@@ -1657,13 +1422,6 @@ __global__ __launch_bounds__(kBlock) void k_engine(EngineArgs a) {
 // explicit instantiations used by fc_capi.hip
 // --------------------------------------------------------------------------------------
 template __global__ void k_sample1<kKeyMag>(const float*, SamplePlan, uint64_t, uint64_t, WsPtrs, uint32_t, fc_packet_hdr*, HdrInit, const fc_encode_job*, uint64_t);
-template __global__ void k_sample1<kKeyPhilox>(const float*, SamplePlan, uint64_t, uint64_t, WsPtrs, uint32_t, fc_packet_hdr*, HdrInit, const fc_encode_job*, uint64_t);
-template __global__ void k_compact<kKeyMag, kPredKey, FC_FMT_IDXVAL>(CompactArgs);
-template __global__ void k_compact<kKeyPhilox, kPredKey, FC_FMT_IDXVAL>(CompactArgs);
-template __global__ void k_compact<kKeyMag, kPredMask, FC_FMT_IDXVAL>(CompactArgs);
-template __global__ void k_compact<kKeyMag, kPredMask, FC_FMT_BITMAP>(CompactArgs);
-template __global__ void k_compact<kKeyMag, kPredBern, FC_FMT_IDXVAL>(CompactArgs);
-template __global__ void k_compact<kKeyMag, kPredBern, FC_FMT_BITMAP>(CompactArgs);
 template __global__ void k_engine<kKeyMag>(EngineArgs);
 template __global__ void k_engine<kKeyPhilox>(EngineArgs);
 

@@ -7,8 +7,11 @@ streams are pinned here (KAT vectors below) and NOT against the reference — "p
 unpinned" w.r.t. the reference for native-RNG mode; the numpy-RNG parity mode is exact.
 
 Stream layout used by the HIP kernels (openmsftl_amd/csrc/fc_common.h):
-  element i  ->  block b = i >> 2,  ctr = (lo32 b, hi32 b, lo32 offset, hi32 offset),
-                 key = (lo32 seed, hi32 seed),  word = philox(ctr, key)[i & 3]
+  codec keys / Bernoulli masks (``element_words``):
+      element i  ->  block b = ((i >> 8) << 6) | (i & 63),  word (i >> 6) & 3
+  QSGD dither (``linear_words``):
+      element i  ->  block b = i >> 2,  word i & 3
+  with ctr = (lo32 b, hi32 b, lo32 offset, hi32 offset), key = (lo32 seed, hi32 seed).
 """
 from __future__ import annotations
 
@@ -48,18 +51,31 @@ def philox4x32_10(c0, c1, c2, c3, k0, k1):
     return c0, c1, c2, c3
 
 
-def element_words(n: int, seed: int, offset: int = 0, start: int = 0) -> np.ndarray:
-    """The 32-bit Philox word the HIP kernels assign to elements ``start .. start+n-1``."""
-    if n == 0:
-        return np.zeros(0, dtype=np.uint32)
-    idx = np.arange(start, start + n, dtype=np.uint64)
-    b = idx >> np.uint64(2)
+def _words(idx: np.ndarray, b: np.ndarray, word: np.ndarray, seed: int, offset: int):
     blocks, inv = np.unique(b, return_inverse=True)
     outs = philox4x32_10(blocks & MASK32, blocks >> np.uint64(32),
                          np.uint32(offset & 0xFFFFFFFF), np.uint32((offset >> 32) & 0xFFFFFFFF),
                          np.uint32(seed & 0xFFFFFFFF), np.uint32((seed >> 32) & 0xFFFFFFFF))
     table = np.stack(outs, axis=1)                      # (nblocks, 4)
-    return table[inv, (idx & np.uint64(3)).astype(np.int64)]
+    return table[inv, word.astype(np.int64)]
+
+
+def element_words(n: int, seed: int, offset: int = 0, start: int = 0) -> np.ndarray:
+    """The 32-bit Philox word the HIP codec assigns to elements ``start .. start+n-1`` (rand-k
+    keys, Bernoulli masks): block ((i >> 8) << 6) | (i & 63), word (i >> 6) & 3."""
+    if n == 0:
+        return np.zeros(0, dtype=np.uint32)
+    idx = np.arange(start, start + n, dtype=np.uint64)
+    b = ((idx >> np.uint64(8)) << np.uint64(6)) | (idx & np.uint64(63))
+    return _words(idx, b, (idx >> np.uint64(6)) & np.uint64(3), seed, offset)
+
+
+def linear_words(n: int, seed: int, offset: int = 0, start: int = 0) -> np.ndarray:
+    """QSGD's dither words: block i >> 2, word i & 3 (fc_qsgd.hip)."""
+    if n == 0:
+        return np.zeros(0, dtype=np.uint32)
+    idx = np.arange(start, start + n, dtype=np.uint64)
+    return _words(idx, idx >> np.uint64(2), idx & np.uint64(3), seed, offset)
 
 
 def bernoulli_threshold(p: float) -> int:

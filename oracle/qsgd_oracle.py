@@ -11,7 +11,7 @@ encoding", NeurIPS 2017).  There is no reference output to pin against: **parity
 with respect to the reference.  This module states the exact arithmetic the HIP codec
 (openmsftl_amd/csrc/fc_qsgd.hip) implements, so the GPU is pinned to it bit for bit:
 
-    U_i   = (philox_word(i) >> 8) * 2**-24          (oracle/philox.py stream layout)
+    U_i   = (linear_word(i) >> 8) * 2**-24          (oracle/philox.py linear_words)
     l_i   = floor(fl64(fl64(s * |g_i|) / norm) + U_i)   in [0, s];  0 if not finite
     code  = signbit(g_i) << (W - 1) | l_i,  W = 4 / 8 / 16 bits for bits <= 2 / 6 / 14
     value = fl32(+-(norm / (s * tau)) * l_i)         (fp64 product, one rounding)
@@ -43,7 +43,7 @@ def norm64(g: np.ndarray) -> float:
 
 def levels_and_signs(g: np.ndarray, bits: int, seed: int, offset: int, norm: float):
     s = float(2 ** bits)
-    u = (ph.element_words(g.shape[0], seed, offset) >> np.uint32(8)).astype(np.float64) * 2.0 ** -24
+    u = (ph.linear_words(g.shape[0], seed, offset) >> np.uint32(8)).astype(np.float64) * 2.0 ** -24
     with np.errstate(invalid="ignore", divide="ignore", over="ignore"):
         r = (s * np.abs(g.astype(np.float64))) / norm
         f = np.floor(r + u)
