@@ -208,10 +208,21 @@ static void launch_compact_mag(const CompactArgs& a, uint32_t m, hipStream_t s) 
   hipLaunchKernelGGL(k_compact_mag1, dim3(a.nchunks, m), dim3(kCBlock), 0, s, a);
 }
 
+// the PredArgs of k_compact_pred from a compaction's CompactArgs
+static PredArgs pred_args(const CompactArgs& a) {
+  PredArgs p;
+  memset(&p, 0, sizeof p);
+  p.g = a.g; p.n = a.n; p.seed = a.seed; p.offset = a.offset; p.bern_thr = a.bern_thr;
+  p.mask = a.mask; p.idx = a.idx; p.val = a.val; p.bitmap = a.bitmap; p.cnt = a.cnt;
+  p.qoff = a.qoff; p.S = a.W.st; p.ccnt = a.W.ccnt; p.cand = a.W.cand; p.jobs = a.jobs;
+  p.ws_stride = a.ws_stride; p.ib = a.ib; p.nonfinite_keep = a.nonfinite_keep;
+  return p;
+}
+
 static int launch_compact_key(int key_mode, const CompactArgs& a, hipStream_t s, uint32_t m = 1) {
   TimedLaunch t(FC_TIME_COMPACT, s);
   if (key_mode == FC_KEY_PHILOX)
-    hipLaunchKernelGGL((k_compact_pred<kSrcPhiloxKey, FC_FMT_IDXVAL>), dim3(a.nchunks, m), dim3(kCBlock), 0, s, a);
+    hipLaunchKernelGGL((k_compact_pred<kSrcPhiloxKey, FC_FMT_IDXVAL>), dim3(a.nchunks, m), dim3(kCBlock), 0, s, pred_args(a));
   else
     launch_compact_mag(a, m, s);
   FC_LAUNCHED("k_compact");
@@ -544,15 +555,21 @@ int fc_mask_encode(const float* g, uint64_t n, int codec, const uint32_t* mask_b
   a.hdr = hdr; a.W = ws_ptrs(ws, n); a.HI = hi;
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid(a.nchunks), blk(kCBlock);
-  TimedLaunch t(FC_TIME_COMPACT, s);
-  if (mask_bits) {
-    if (format == FC_FMT_BITMAP) hipLaunchKernelGGL((k_compact_pred<kSrcMaskBits, FC_FMT_BITMAP>), grid, blk, 0, s, a);
-    else hipLaunchKernelGGL((k_compact_pred<kSrcMaskBits, FC_FMT_IDXVAL>), grid, blk, 0, s, a);
-  } else {
-    if (format == FC_FMT_BITMAP) hipLaunchKernelGGL((k_compact_pred<kSrcBern, FC_FMT_BITMAP>), grid, blk, 0, s, a);
-    else hipLaunchKernelGGL((k_compact_pred<kSrcBern, FC_FMT_IDXVAL>), grid, blk, 0, s, a);
+  const PredArgs pa = pred_args(a);
+  {
+    TimedLaunch t(FC_TIME_COMPACT, s);
+    if (mask_bits) {
+      if (format == FC_FMT_BITMAP) hipLaunchKernelGGL((k_compact_pred<kSrcMaskBits, FC_FMT_BITMAP>), grid, blk, 0, s, pa);
+      else hipLaunchKernelGGL((k_compact_pred<kSrcMaskBits, FC_FMT_IDXVAL>), grid, blk, 0, s, pa);
+    } else {
+      if (format == FC_FMT_BITMAP) hipLaunchKernelGGL((k_compact_pred<kSrcBern, FC_FMT_BITMAP>), grid, blk, 0, s, pa);
+      else hipLaunchKernelGGL((k_compact_pred<kSrcBern, FC_FMT_IDXVAL>), grid, blk, 0, s, pa);
+    }
+    FC_LAUNCHED("k_compact_pred(mask)");
   }
-  FC_LAUNCHED("k_compact(mask)");
+  // the packet's static header (its only writer; decoders read it after this stream point)
+  hipLaunchKernelGGL(k_write_hdr, dim3(1), dim3(64), 0, s, hdr, hi);
+  FC_LAUNCHED("k_write_hdr");
   return FC_OK;
 }
 

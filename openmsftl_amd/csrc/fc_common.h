@@ -61,8 +61,11 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
     if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
-    const uint32_t lo0 = c.x * 0xD2511F53u, hi0 = __umulhi(c.x, 0xD2511F53u);
-    const uint32_t lo1 = c.z * 0xCD9E8D57u, hi1 = __umulhi(c.z, 0xCD9E8D57u);
+    // one 32 x 32 -> 64 multiply per product (v_mad_u64_u32) instead of mul_lo + mul_hi: the
+    // integer multiplies are quarter-rate and set the cost of every Philox-driven pass
+    const uint64_t p0 = (uint64_t)c.x * 0xD2511F53ull, p1 = (uint64_t)c.z * 0xCD9E8D57ull;
+    const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
+    const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
     c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
   }
   return c;

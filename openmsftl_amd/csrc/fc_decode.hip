@@ -749,10 +749,7 @@ __global__ __launch_bounds__(kQBlock, 4) void k_fold_q(DecodeArgs a) {
     const uint32_t en = q == 3 ? (uint32_t)(v >> 48) : (uint32_t)(v >> (16 * q)) & 0xffffu;
     return en - st;
   };
-  // (the last chunk too: the fast body reads up to 255 entries past a quarter's end without a
-  // clamp, which stays inside the packet only while a next chunk's slot follows)
-  const bool dense_q = __any(qcount(qo0) > (uint32_t)(kQTail * 64) || qcount(qo1) > (uint32_t)(kQTail * 64)) ||
-                       c + 1u == gridDim.x;
+  const bool dense_q = __any(qcount(qo0) > (uint32_t)(kQTail * 64) || qcount(qo1) > (uint32_t)(kQTail * 64));
   auto range = [&](uint32_t m, uint32_t& st, uint32_t& en) {   // uniform
     const uint64_t src = m < 64 ? qo0 : qo1;
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)src, (int)(m & 63));
@@ -809,10 +806,9 @@ __global__ __launch_bounds__(kQBlock, 4) void k_fold_q(DecodeArgs a) {
     // compare and comp >= T64 in float form:
     //     comp >= T64  <=>  !(|v| <= Tf)  ||  (|v| == Tf && lc >= Ti - chunk base)
     // (Tf = T64's key as a float; NaN is unordered -> kept, its key is above every finite T).
-    // The entry loads are not clamped: lanes past the quarter's end read the next entries of
-    // the packet (the last chunk takes the slow body), are never written, and their tile read
-    // is masked into the quarter.  (Round 2's form — clamped loads, 64-bit comps and a branch
-    // per read — spent 34 VALU lane-ops per entry; the fold was VALU-bound.)
+    // Lanes past the item's end re-read its last entry and are never written; every tile read
+    // is masked into the quarter.  (Round 2's form — 64-bit comps and a branch per read —
+    // spent 34 VALU lane-ops per entry.)
     uint32_t ids_[2][kQGroup][kQR];
     float vs_[2][kQGroup][kQR];
     uint32_t qn_[2][kQGroup];                                   // the item's entries (uniform)
@@ -826,10 +822,14 @@ __global__ __launch_bounds__(kQBlock, 4) void k_fold_q(DecodeArgs a) {
         const QMeta& pm = s_meta[m];
         gf32* val = (gf32*)uni_ptr(pm.val) + base + st;
         gu16* idx = (gu16*)uni_ptr(pm.idx) + base + st;
+        // lanes past the item's end re-read its last entry (one address, no extra traffic:
+        // unclamped loads of the next entries cost +25 % bytes, 19.4 against 17.6 us/packet)
+        const uint32_t last = en > st ? en - st - 1u : 0u;
 #pragma unroll
         for (int r = 0; r < kQR; ++r) {
-          vs_[sl][d][r] = val[lane + r * 64];
-          ids_[sl][d][r] = idx[lane + r * 64];
+          const uint32_t e = min((uint32_t)(lane + r * 64), last);
+          vs_[sl][d][r] = val[e];
+          ids_[sl][d][r] = idx[e];
         }
       }
     };

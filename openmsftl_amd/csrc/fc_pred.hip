@@ -62,50 +62,77 @@ __global__ __launch_bounds__(64) void k_setup_bracket(SetupArgs a) {
   }
 }
 
-template <int SRC, int FMT>
-__global__ __launch_bounds__(kCBlock, FC_MAG1_WAVES_PER_EU) void k_compact_pred(CompactArgs a0) {
-  __shared__ __attribute__((aligned(16))) PredShared sh;
+// Arguments of k_compact_pred: only what the pass reads (CompactArgs' header-init block and
+// unused pointers, hoisted into SGPRs at entry, spilled ~180 SGPRs).  Mask pipelines write
+// their static header with k_write_hdr after the pass.
+struct PredArgs {
+  const float* g;
+  uint64_t n, seed, offset, bern_thr;
+  const uint32_t* mask;
+  uint16_t* idx;
+  float* val;
+  uint32_t* bitmap;
+  uint32_t* cnt;
+  uint64_t* qoff;
+  TopkState* S;              // rand-k: encoder state (bracket, totals), candidate slots
+  uint32_t* ccnt;
+  uint64_t* cand;
+  const fc_encode_job* jobs; // batched rand-k: client blockIdx.y
+  uint64_t ws_stride;
+  uint32_t ib, nonfinite_keep;
+};
+
+__global__ __launch_bounds__(64) void k_write_hdr(fc_packet_hdr* hdr, HdrInit HI) {
+  if (threadIdx.x == 0) write_hdr_static(hdr, HI);
+}
+
+// FULL: the whole chunk is in range — non-temporal loads at immediate offsets and the host
+// mask read as one 64-bit scalar load per group (its two words ARE the group's keep mask);
+// the last, partial chunk clamps its addresses and reads the mask per lane.  (One body for
+// both let hipcc merge the two load forms into per-lane 64-bit addresses without the NT hint.)
+template <int SRC, int FMT, bool FULL>
+__device__ __forceinline__ void pred_body(const PredArgs& a, uint32_t chunk, PredShared& sh) {
   constexpr int NW = kCWaves, NQ = MagGeo<NW>::kQ, NI = NQ / 4;
   static_assert(NQ == 16, "16 elements per lane");
   const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
-  const uint32_t chunk = blockIdx.x, client = blockIdx.y;
-  const MagOut o = mag_out(a0, client);
-  uint64_t seed = a0.seed, offset = a0.offset;
-  fc_packet_hdr* hdr = a0.hdr;
-  if (a0.jobs) {
-    const fc_u32x4 so = sload4(&a0.jobs[client].seed);
-    seed = ((uint64_t)so.y << 32) | so.x;
-    offset = ((uint64_t)so.w << 32) | so.z;
-  }
-  float x[NQ];
-  mag_load<NW>(o.g, chunk, a0.n, x);
   const uint32_t base = chunk * (uint32_t)kChunk;
-  const uint32_t n32 = (uint32_t)a0.n;
+  const uint32_t n32 = (uint32_t)a.n;
   const uint32_t lbase = (uint32_t)(w * 256 + lane);
+  float x[NQ];
+  {
+    typedef __attribute__((address_space(1))) const float gf;
+    if (FULL) {
+      gf* gp = (gf*)a.g + base + lbase;
+#pragma unroll
+      for (int q = 0; q < NQ; ++q)
+        x[q] = __builtin_nontemporal_load(gp + (q >> 2) * MagGeo<NW>::kIStride + (q & 3) * 64);
+    } else {
+      const uint32_t lastl = n32 - 1u - base;
+#pragma unroll
+      for (int q = 0; q < NQ; ++q)
+        x[q] = ((gf*)a.g)[base + min(lbase + (q >> 2) * MagGeo<NW>::kIStride + (q & 3) * 64, lastl)];
+    }
+  }
 #define FC_LOC(q) (lbase + ((q) >> 2) * MagGeo<NW>::kIStride + ((q) & 3) * 64)
-  if (SRC != kSrcPhiloxKey && a0.write_hdr && chunk == 0 && tid == 0)
-    write_hdr_static(hdr, a0.HI);                  // mask pipelines: the header's one writer
-
   // ---- predicates: bit q of pb (listed), cb (candidate), nb (NaN stand-in) ---------------
   uint32_t Lk = 0, Li = 0, t_lo = 0, t_hi = 0, cand_on = 0;
   if (SRC == kSrcPhiloxKey) {
-    const MagState st = mag_state(o.S);
+    const MagState st = mag_state(a.S);
     const bool none = st.L64 == kSelectNothing;
-    Lk = none ? 0xffffffffu : (uint32_t)(st.L64 >> o.ib);
-    Li = none ? 0xffffffffu : (uint32_t)(st.L64 & ((1ull << o.ib) - 1));
+    Lk = none ? 0xffffffffu : (uint32_t)(st.L64 >> a.ib);
+    Li = none ? 0xffffffffu : (uint32_t)(st.L64 & ((1ull << a.ib) - 1));
     t_lo = st.t_lo; t_hi = st.t_hi; cand_on = st.cand_on;
   }
+  const uint64_t seg0 = ((uint64_t)base >> 8) + (uint32_t)w;
   uint32_t pb = 0, cb = 0, nb = 0;
-#pragma unroll
-  for (int i = 0; i < NI; ++i) {
+  auto preds = [&](int i) {
     uint4 r = make_uint4(0u, 0u, 0u, 0u);
-    if (SRC != kSrcMaskBits)
-      r = philox_seg(((uint64_t)base >> 8) + (uint32_t)(i * NW + w), (uint32_t)lane, seed, offset);
+    if (SRC != kSrcMaskBits) r = philox_seg(seg0 + (uint32_t)(i * NW), (uint32_t)lane, a.seed, a.offset);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int q = i * 4 + j;
       const uint32_t e = base + FC_LOC(q);
-      const bool valid = e < n32;
+      const bool valid = FULL || e < n32;
       const uint32_t word = j == 0 ? r.x : j == 1 ? r.y : j == 2 ? r.z : r.w;
       bool p, c = false, nf = false;
       if (SRC == kSrcPhiloxKey) {
@@ -114,9 +141,19 @@ __global__ __launch_bounds__(kCBlock, FC_MAG1_WAVES_PER_EU) void k_compact_pred(
         c = valid & (cand_on != 0) & (key >= t_lo) & (key <= t_hi);
       } else {
         bool keep;
-        if (SRC == kSrcMaskBits) keep = valid && ((a0.mask[e >> 5] >> (e & 31)) & 1u) != 0;
-        else keep = (uint64_t)word < a0.bern_thr;
-        nf = a0.nonfinite_keep && !keep && (__float_as_uint(x[q]) & 0x7fffffffu) >= 0x7f800000u;
+        if (SRC == kSrcMaskBits) {
+          if (FULL) {                                  // the group's 64 keep bits, scalar
+            typedef __attribute__((address_space(4))) const uint64_t cu64;
+            const uint32_t wu = (uint32_t)__builtin_amdgcn_readfirstlane(w);
+            const uint64_t m64 = ((cu64*)a.mask)[(base >> 6) + (uint32_t)(i * 32 + j) + wu * 4u];
+            keep = ((m64 >> lane) & 1ull) != 0;
+          } else {
+            keep = valid && ((a.mask[e >> 5] >> (e & 31)) & 1u) != 0;
+          }
+        } else {
+          keep = (uint64_t)word < a.bern_thr;
+        }
+        nf = a.nonfinite_keep && !keep && (__float_as_uint(x[q]) & 0x7fffffffu) >= 0x7f800000u;
         p = valid & (keep | nf);
         nf = nf & valid;
       }
@@ -124,6 +161,14 @@ __global__ __launch_bounds__(kCBlock, FC_MAG1_WAVES_PER_EU) void k_compact_pred(
       cb |= (uint32_t)c << q;
       nb |= (uint32_t)nf << q;
     }
+  };
+  if (SRC == kSrcPhiloxKey) {
+    // one Philox block at a time (unrolled, hipcc interleaved the four and needed 89 VGPRs)
+#pragma unroll 1
+    for (int i = 0; i < NI; ++i) preds(i);
+  } else {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) preds(i);
   }
   // ---- phase 1: group counts (scalar popcounts), every wave scans the 32 words itself -----
   uint32_t pk[NI];
@@ -154,9 +199,6 @@ __global__ __launch_bounds__(kCBlock, FC_MAG1_WAVES_PER_EU) void k_compact_pred(
     const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)((q & 2) ? o23 : o01), (q >> 2) * NW + w);
     return (q & 1) ? v >> 16 : v & 0xffffu;
   };
-  auto value = [&](int q) -> float {
-    return ((nb >> q) & 1u) ? __uint_as_float(0x7fc00000u) : x[q];
-  };
   // ---- phase 2: listed entries -> LDS stage (or straight to the slot); bitmap words -------
   const uint64_t slot = base;
   const bool staged = tot_e <= (uint32_t)kStage;   // block-uniform
@@ -166,30 +208,38 @@ __global__ __launch_bounds__(kCBlock, FC_MAG1_WAVES_PER_EU) void k_compact_pred(
     const uint64_t m = __ballot(p);
     const uint32_t pos = prefix_count(m) + goff_of(q);
     if (FMT == FC_FMT_BITMAP && lane < 2)          // the group's two bitmap words
-      a0.bitmap[(base + FC_LOC(q) - (uint32_t)lane) / 32 + (uint32_t)lane] = (uint32_t)(m >> (32 * lane));
+      a.bitmap[(base + FC_LOC(q) - (uint32_t)lane) / 32 + (uint32_t)lane] = (uint32_t)(m >> (32 * lane));
+    const float v = ((nb >> q) & 1u) ? __uint_as_float(0x7fc00000u) : x[q];
     if (p) {
       if (staged) {
-        sh.st[pos] = make_uint2(FC_LOC(q), __float_as_uint(value(q)));
+        sh.st[pos] = make_uint2(FC_LOC(q), __float_as_uint(v));
       } else {
-        if (FMT == FC_FMT_IDXVAL) o.idx[slot + pos] = (uint16_t)FC_LOC(q);
-        o.val[slot + pos] = value(q);
+        if (FMT == FC_FMT_IDXVAL) a.idx[slot + pos] = (uint16_t)FC_LOC(q);
+        a.val[slot + pos] = v;
       }
     }
   }
-  // ---- candidates (rand-k): wave w's LDS sub-slot at a wave-uniform running count ---------
+  // ---- candidates (rand-k): wave w's LDS sub-slot at a wave-uniform running count; the key
+  // is recomputed (one Philox block per segment that holds a candidate: rare) ---------------
   constexpr int kCW = kCandSlot / NW;
   uint32_t wc = 0;
   if (SRC == kSrcPhiloxKey && cand_on) {
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const bool c = (cb >> q) & 1u;
-      const uint64_t mc = __ballot(c);
-      const uint32_t pos = wc + prefix_count(mc);
-      if (c && pos < (uint32_t)kCW) {
-        const uint32_t e = base + FC_LOC(q);
-        sh.cst[w * kCW + pos] = comp_of(philox_word(e, seed, offset) >> 1, e, o.ib);
+    for (int i = 0; i < NI; ++i) {
+      if (!__any((cb >> (i * 4)) & 0xfu)) continue;   // uniform
+      const uint4 r = philox_seg(seg0 + (uint32_t)(i * NW), (uint32_t)lane, a.seed, a.offset);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int q = i * 4 + j;
+        const bool c = (cb >> q) & 1u;
+        const uint64_t mc = __ballot(c);
+        const uint32_t pos = wc + prefix_count(mc);
+        if (c && pos < (uint32_t)kCW) {
+          const uint32_t word = j == 0 ? r.x : j == 1 ? r.y : j == 2 ? r.z : r.w;
+          sh.cst[w * kCW + pos] = comp_of(word >> 1, base + FC_LOC(q), a.ib);
+        }
+        wc += (uint32_t)__popcll(mc);
       }
-      wc += (uint32_t)__popcll(mc);
     }
   }
   if (lane == 0) sh.wcnt[w] = wc;
@@ -204,13 +254,13 @@ __global__ __launch_bounds__(kCBlock, FC_MAG1_WAVES_PER_EU) void k_compact_pred(
     c_ovf |= wn[j] > (uint32_t)kCW;
   }
   if (tid == 0) {
-    o.cnt[chunk] = tot_e;
-    if (FMT == FC_FMT_IDXVAL && o.qoff)
-      o.qoff[chunk] = qs1 | ((uint64_t)qs2 << 16) | ((uint64_t)qs3 << 32) | ((uint64_t)tot_e << 48);
+    a.cnt[chunk] = tot_e;
+    if (FMT == FC_FMT_IDXVAL && a.qoff)
+      a.qoff[chunk] = qs1 | ((uint64_t)qs2 << 16) | ((uint64_t)qs3 << 32) | ((uint64_t)tot_e << 48);
     if (SRC == kSrcPhiloxKey) {
-      o.ccnt[chunk] = c_ovf ? max(tot_c, (uint32_t)kCandSlot + 1u) : tot_c;
-      atomicAdd(&o.S->shard_ent[chunk % kShards], tot_e);
-      if (tot_c) atomicAdd(&o.S->shard_cnd[chunk % kShards], tot_c);
+      a.ccnt[chunk] = c_ovf ? max(tot_c, (uint32_t)kCandSlot + 1u) : tot_c;
+      atomicAdd(&a.S->shard_ent[chunk % kShards], tot_e);
+      if (tot_c) atomicAdd(&a.S->shard_cnd[chunk % kShards], tot_c);
     }
   }
   if (staged) {                                    // coalesced 16-B stores of the staged slot
@@ -219,12 +269,12 @@ __global__ __launch_bounds__(kCBlock, FC_MAG1_WAVES_PER_EU) void k_compact_pred(
         const uint4 p0 = *reinterpret_cast<const uint4*>(&sh.st[t]);
         const uint4 p1 = *reinterpret_cast<const uint4*>(&sh.st[t + 2]);
         if (FMT == FC_FMT_IDXVAL)
-          *reinterpret_cast<uint2*>(o.idx + slot + t) = make_uint2(p0.x | (p0.z << 16), p1.x | (p1.z << 16));
-        *reinterpret_cast<uint4*>(o.val + slot + t) = make_uint4(p0.y, p0.w, p1.y, p1.w);
+          *reinterpret_cast<uint2*>(a.idx + slot + t) = make_uint2(p0.x | (p0.z << 16), p1.x | (p1.z << 16));
+        *reinterpret_cast<uint4*>(a.val + slot + t) = make_uint4(p0.y, p0.w, p1.y, p1.w);
       } else {
         for (uint32_t u = t; u < tot_e; ++u) {
-          if (FMT == FC_FMT_IDXVAL) o.idx[slot + u] = (uint16_t)sh.st[u].x;
-          o.val[slot + u] = __uint_as_float(sh.st[u].y);
+          if (FMT == FC_FMT_IDXVAL) a.idx[slot + u] = (uint16_t)sh.st[u].x;
+          a.val[slot + u] = __uint_as_float(sh.st[u].y);
         }
       }
     }
@@ -238,14 +288,43 @@ __global__ __launch_bounds__(kCBlock, FC_MAG1_WAVES_PER_EU) void k_compact_pred(
       if ((uint32_t)j < wj) pre += m;
       if ((uint32_t)j == wj) nj = m;
     }
-    if (p < nj) o.cand[(uint64_t)chunk * kCandSlot + pre + p] = sh.cst[tid];
+    if (p < nj) a.cand[(uint64_t)chunk * kCandSlot + pre + p] = sh.cst[tid];
   }
 }
 
-template __global__ void k_compact_pred<kSrcPhiloxKey, FC_FMT_IDXVAL>(CompactArgs);
-template __global__ void k_compact_pred<kSrcMaskBits, FC_FMT_IDXVAL>(CompactArgs);
-template __global__ void k_compact_pred<kSrcMaskBits, FC_FMT_BITMAP>(CompactArgs);
-template __global__ void k_compact_pred<kSrcBern, FC_FMT_IDXVAL>(CompactArgs);
-template __global__ void k_compact_pred<kSrcBern, FC_FMT_BITMAP>(CompactArgs);
+// rand-k's occupancy (its Philox rounds, unrolled four at a time, once spilled 39 VGPRs)
+#ifndef FC_PRED_PHILOX_WAVES
+#define FC_PRED_PHILOX_WAVES 8
+#endif
+template <int SRC, int FMT>
+__global__ __launch_bounds__(kCBlock, SRC == kSrcPhiloxKey ? FC_PRED_PHILOX_WAVES : FC_MAG1_WAVES_PER_EU) void k_compact_pred(PredArgs a) {
+  __shared__ __attribute__((aligned(16))) PredShared sh;
+  const uint32_t chunk = blockIdx.x;
+  if (a.jobs) {                                    // batched rand-k: client blockIdx.y
+    const uint32_t client = blockIdx.y;
+    const fc_u32x8 v = sload8(&a.jobs[client]);    // {g, idx, val, cnt}
+    a.g = as_ptr<const float>(v[0], v[1]); a.idx = as_ptr<uint16_t>(v[2], v[3]);
+    a.val = as_ptr<float>(v[4], v[5]); a.cnt = as_ptr<uint32_t>(v[6], v[7]);
+    const fc_u32x4 so = sload4(&a.jobs[client].seed);
+    a.seed = ((uint64_t)so.y << 32) | so.x;
+    a.offset = ((uint64_t)so.w << 32) | so.z;
+    const fc_u32x2 qv = sload2(&a.jobs[client].qoff);
+    a.qoff = as_ptr<uint64_t>(qv.x, qv.y);
+    const uint64_t sh_b = (uint64_t)client * a.ws_stride;
+    a.S = reinterpret_cast<TopkState*>(reinterpret_cast<char*>(a.S) + sh_b);
+    a.ccnt = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(a.ccnt) + sh_b);
+    a.cand = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(a.cand) + sh_b);
+  }
+  if ((uint64_t)chunk * kChunk + kChunk <= a.n)    // block-uniform
+    pred_body<SRC, FMT, true>(a, chunk, sh);
+  else
+    pred_body<SRC, FMT, false>(a, chunk, sh);
+}
+
+template __global__ void k_compact_pred<kSrcPhiloxKey, FC_FMT_IDXVAL>(PredArgs);
+template __global__ void k_compact_pred<kSrcMaskBits, FC_FMT_IDXVAL>(PredArgs);
+template __global__ void k_compact_pred<kSrcMaskBits, FC_FMT_BITMAP>(PredArgs);
+template __global__ void k_compact_pred<kSrcBern, FC_FMT_IDXVAL>(PredArgs);
+template __global__ void k_compact_pred<kSrcBern, FC_FMT_BITMAP>(PredArgs);
 
 }  // namespace fc
