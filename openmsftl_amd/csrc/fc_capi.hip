@@ -815,7 +815,7 @@ static int mask_dense64(const T* g, uint64_t n, int codec, const uint32_t* mask_
   const int mode = codec == FC_CODEC_RAND ? 0 : codec == FC_CODEC_DROPOUT_BIASED ? 1 : 2;
   hipStream_t s = (hipStream_t)stream;
   TimedLaunch t(FC_TIME_COMPACT, s);
-  hipLaunchKernelGGL(k_mask_dense64<T>, dim3(grid_of(n)), dim3(kBlock), 0, s, g, n, mask_bits,
+  hipLaunchKernelGGL(k_mask_dense64<T>, dim3(grid_of((n + 3) / 4)), dim3(kBlock), 0, s, g, n, mask_bits,
                      (uint64_t)thr, seed, offset, mode, p, out);
   FC_LAUNCHED("k_mask_dense64");
   return FC_OK;

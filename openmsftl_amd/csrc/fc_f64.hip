@@ -232,25 +232,37 @@ __device__ __forceinline__ double x86_div(double a, double b) {
 //   mode 2 ('dropout-unbiased'): q = (g * double(keep)) / p        (compression.py:59-60)
 // T = float: a float32 gradient promoted exactly (NumPy's float32 * int64 mask -> float64), so
 // fp32 'dropout-*' also reproduces g * 0 = -0.0 for negative g and the x86 NaN rules.
+// Thread = (256-element segment, lane): elements seg*256 + j*64 + lane, j = 0..3 — the four
+// words of ONE Philox block (fc_common.h's element map), coalesced across the wave.
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_mask_dense64(const T* __restrict__ g, uint64_t n,
                                                          const uint32_t* __restrict__ mask,
                                                          uint64_t bern_thr, uint64_t seed,
                                                          uint64_t off, int mode, double p,
                                                          double* out) {
+  const uint64_t slots = (n + 255) / 256 * 64;
   const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
-    const bool keep = mask ? ((mask[i >> 5] >> (i & 31)) & 1u) != 0
-                           : (uint64_t)philox_word(i, seed, off) < bern_thr;
-    const double x = (double)g[i];
-    double q;
-    if (mode == 0) {
-      q = keep ? x : 0.0;
-    } else {
-      q = x86_mul(x, keep ? 1.0 : 0.0);
-      if (mode == 2) q = x86_div(q, p);
+  for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < slots; t += stride) {
+    const uint64_t seg = t >> 6;
+    const uint32_t lane = (uint32_t)(t & 63);
+    uint4 r = make_uint4(0u, 0u, 0u, 0u);
+    if (!mask) r = philox_seg(seg, lane, seed, off);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint64_t i = seg * 256 + (uint64_t)j * 64 + lane;
+      if (i >= n) break;
+      const uint32_t word = j == 0 ? r.x : j == 1 ? r.y : j == 2 ? r.z : r.w;
+      const bool keep = mask ? ((mask[i >> 5] >> (i & 31)) & 1u) != 0 : (uint64_t)word < bern_thr;
+      const double x = (double)g[i];
+      double q;
+      if (mode == 0) {
+        q = keep ? x : 0.0;
+      } else {
+        q = x86_mul(x, keep ? 1.0 : 0.0);
+        if (mode == 2) q = x86_div(q, p);
+      }
+      out[i] = q;
     }
-    out[i] = q;
   }
 }
 

@@ -564,10 +564,11 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
   const uint32_t incl = wave_incl_scan(sum4);
   const uint32_t tot_e = (uint32_t)__builtin_amdgcn_readlane((int)incl, kMGroups / 4 - 1);
   const uint32_t e0 = incl - sum4;
-  // quarter q of the chunk = words (q, w): its entries start where word (q, 0) does
-  const uint32_t qs1 = (uint32_t)__builtin_amdgcn_readlane((int)e0, 1 * NW);
-  const uint32_t qs2 = (uint32_t)__builtin_amdgcn_readlane((int)e0, 2 * NW);
-  const uint32_t qs3 = (uint32_t)__builtin_amdgcn_readlane((int)e0, 3 * NW);
+  // word L covers elements [256 L, 256 L + 256) of the chunk (i * NW + w = element / 256), so
+  // quarter q (2048 elements) starts where word 8 q does
+  const uint32_t qs1 = (uint32_t)__builtin_amdgcn_readlane((int)e0, 8);
+  const uint32_t qs2 = (uint32_t)__builtin_amdgcn_readlane((int)e0, 16);
+  const uint32_t qs3 = (uint32_t)__builtin_amdgcn_readlane((int)e0, 24);
   const uint32_t e1 = e0 + (word & 0xffu), e2 = e1 + ((word >> 8) & 0xffu);
   const uint32_t e3 = e2 + ((word >> 16) & 0xffu);
   const uint32_t o01 = e0 | (e1 << 16), o23 = e2 | (e3 << 16);
@@ -935,9 +936,9 @@ union FusedShared {
 #ifndef FC_DENSE_PKT
 #define FC_DENSE_PKT 0        // 1: the dense path also writes every packet entry (A/B only)
 #endif
-template <bool DENSE>
-__global__ __launch_bounds__(kCBlock, FC_MAG1_WAVES_PER_EU) void k_fused_mag(CompactArgs a0, SamplePlan P,
-                                                                              HdrInit HI, uint32_t nsamp) {
+template <bool DENSE, int NW>
+__device__ __forceinline__ void fused_mag_wg(const CompactArgs& a0, const SamplePlan& P,
+                                             const HdrInit& HI, uint32_t nsamp) {
   __shared__ __attribute__((aligned(16))) FusedShared u;
   __shared__ MagState s_st;
   TopkState* S = a0.W.st;
@@ -948,8 +949,8 @@ __global__ __launch_bounds__(kCBlock, FC_MAG1_WAVES_PER_EU) void k_fused_mag(Com
     return;
   }
   const uint32_t chunk = blockIdx.x - nsamp;
-  float x[MagGeo<8>::kQ];
-  mag_load<8>(a0.g, chunk, a0.n, x);
+  float x[MagGeo<NW>::kQ];
+  mag_load<NW>(a0.g, chunk, a0.n, x);
   FC_TR(24);
   if (threadIdx.x == 0) {
     uint32_t it = 0;
@@ -965,8 +966,13 @@ __global__ __launch_bounds__(kCBlock, FC_MAG1_WAVES_PER_EU) void k_fused_mag(Com
   FC_TR(25);
   const MagState st = s_st;
   constexpr bool kBin = DENSE ? FC_FUSED_BIN_DENSE != 0 : FC_FUSED_BIN_PKT != 0;
-  compact_mag_item<8, MagShared, DENSE, kBin, !DENSE || FC_DENSE_PKT != 0>(a0, mag_out(a0, 0u), chunk, st, x, u.m);
+  compact_mag_item<NW, MagShared, DENSE, kBin, !DENSE || FC_DENSE_PKT != 0>(a0, mag_out(a0, 0u), chunk, st, x, u.m);
   FC_TR(26);
+}
+template <bool DENSE>
+__global__ __launch_bounds__(kCBlock, FC_MAG1_WAVES_PER_EU) void k_fused_mag(CompactArgs a0, SamplePlan P,
+                                                                              HdrInit HI, uint32_t nsamp) {
+  fused_mag_wg<DENSE, 8>(a0, P, HI, nsamp);
 }
 template __global__ void k_fused_mag<false>(CompactArgs, SamplePlan, HdrInit, uint32_t);
 template __global__ void k_fused_mag<true>(CompactArgs, SamplePlan, HdrInit, uint32_t);
