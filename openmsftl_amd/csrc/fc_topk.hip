@@ -948,6 +948,8 @@ __device__ __forceinline__ void fused_mag_wg(const CompactArgs& a0, const Sample
     sample_body<kKeyMag, true>(a0.g, P, 0ull, 0ull, a0.W, a0.ib, a0.hdr, HI, blockIdx.x, nsamp, true, u.s, pub);
     return;
   }
+  // (chunks in dispatch order: spreading the resident ones over 8 / 64 address streams, as
+  // the batched pass interleaves clients, measured 147 -> 155 / 164 us for a 128 M packet)
   const uint32_t chunk = blockIdx.x - nsamp;
   float x[MagGeo<NW>::kQ];
   mag_load<NW>(a0.g, chunk, a0.n, x);
