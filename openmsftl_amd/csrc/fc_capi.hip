@@ -573,6 +573,9 @@ int fc_mask_encode(const float* g, uint64_t n, int codec, const uint32_t* mask_b
   return FC_OK;
 }
 
+#ifndef FC_DEC_Q
+#define FC_DEC_Q 1
+#endif
 int fc_decode_dense(const fc_packet_view* pkt, int format, uint64_t n, void* out, int out_f64,
                     fc_stream_t stream) {
   FC_CHECK(pkt && out, "NULL argument");
@@ -592,6 +595,11 @@ int fc_decode_dense(const fc_packet_view* pkt, int format, uint64_t n, void* out
     if (out_f64) hipLaunchKernelGGL((k_decode<FC_FMT_IDXVAL, false, true>), grid, blk, 0, s, a);
     // dense decode: 4 resident WGs per CU (no fold counters in LDS); 1024 WGs measured 3 %
     // faster than 768 and 14 % faster than one WG per chunk
+    // dense decode: the quarter-owned waves of the fold (no barrier per chunk): 87.5 us at
+    // 128 M against 109.5 for k_decode_sparse<false> and its per-chunk workgroup barriers
+    // (at 16 M the barrier form is 0.5 us faster: 2048 one-chunk workgroups in ~2 rounds)
+    else if (FC_DEC_Q && num_chunks(n) >= 4096u)
+      hipLaunchKernelGGL((k_fold_q<false, true>), dim3(num_chunks(n)), dim3(kQBlock), 0, s, a);
     else hipLaunchKernelGGL(k_decode_sparse<false>, dim3(decode_grid(n, 4)), dim3(kSBlock), 0, s, a);
   } else {
     if (out_f64) hipLaunchKernelGGL((k_decode<FC_FMT_BITMAP, false, true>), grid, blk, 0, s, a);

@@ -696,15 +696,19 @@ constexpr uint64_t kQWhole = 1ull << 63;        // never set in real offsets (cn
 
 // One entry of a packet folded into the quarter tile with the full per-entry rules (the slow
 // body): rand-k (Philox keys) slack filter, dropout-unbiased fl32(fl64(v)/p) scaling.
+template <bool DEC>
 __device__ __forceinline__ void fold_q_entry(const PktCache& pk, float w, float* qt,
                                              uint32_t qbase, uint32_t id, float v) {
   if (!entry_kept(pk, id, v)) return;
   const float x = pk.codec == FC_CODEC_DROPOUT_UNBIASED ? (float)((double)v / pk.p) : v;
   const uint32_t loc = id - qbase;
-  if (loc < (uint32_t)kQuarter) qt[loc] = __fadd_rn(qt[loc], __fmul_rn(x, w));
+  if (loc < (uint32_t)kQuarter) qt[loc] = DEC ? x : __fadd_rn(qt[loc], __fmul_rn(x, w));
 }
 
-template <bool ACC_IN>
+// DEC: the dense decode of ONE packet with the same quarter-owned waves (no workgroup barrier
+// per chunk): the tile starts at the packet's dropped value (+0, or NaN for dropout-unbiased
+// with p = 0) and every kept entry is ASSIGNED, tile[loc] = v (-0.0 kept), instead of folded.
+template <bool ACC_IN, bool DEC = false>
 __global__ __launch_bounds__(kQBlock, 4) void k_fold_q(DecodeArgs a) {
   __shared__ __attribute__((aligned(16))) float tile[kChunk];
   __shared__ QMeta s_meta[kSparseMaxM];
@@ -719,7 +723,7 @@ __global__ __launch_bounds__(kQBlock, 4) void k_fold_q(DecodeArgs a) {
   s_mark[q][lane] = 0u;
   __syncthreads();
   if (tid < (int)M) {
-    const fc_packet_view v = a.views[tid];
+    const fc_packet_view v = DEC ? a.one : a.views[tid];
     const fc_packet_hdr* h = v.hdr;
     QMeta d;
     d.idx = v.idx; d.val = v.val; d.hdr = h;
@@ -771,10 +775,15 @@ __global__ __launch_bounds__(kQBlock, 4) void k_fold_q(DecodeArgs a) {
   };
   // ---- tile init: +0 (np.sum's start) or the partial sum being continued ----
   float* qt = tile + q * kQuarter;
+  float dz0 = 0.f;                                  // DEC: the dropped coordinates' value
+  if (DEC) {
+    const fc_packet_hdr* h = (const fc_packet_hdr*)uni_ptr(s_meta[0].hdr);
+    if (h->codec == FC_CODEC_DROPOUT_UNBIASED && h->p == 0.0) dz0 = __uint_as_float(0x7fc00000u);
+  }
 #pragma unroll
   for (int i = 0; i < kQuarter / 256; ++i) {
     const uint32_t loc = (uint32_t)(i * 256 + lane * 4);
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 v = make_float4(dz0, dz0, dz0, dz0);
     if (ACC_IN) v = load4(reinterpret_cast<const float*>(a.out), (uint64_t)qbase + loc, a.n);
     *reinterpret_cast<float4*>(&qt[loc]) = v;
   }
@@ -794,7 +803,7 @@ __global__ __launch_bounds__(kQBlock, 4) void k_fold_q(DecodeArgs a) {
       const float w = __uint_as_float(uni32(__float_as_uint(pm.w)));
       gu16* pidx = (gu16*)uni_ptr(pm.idx) + base;
       gf32* pval = (gf32*)uni_ptr(pm.val) + base;
-      if ((uni32(pm.flags) >> 24) & 1u) {       // poisoning: NaN where this packet folds nothing
+      if (!DEC && ((uni32(pm.flags) >> 24) & 1u)) {   // poisoning: NaN where this packet folds nothing
         for (uint32_t e = st + lane; e < en; e += 64) {
           const uint32_t id = (uint32_t)base + pidx[e];
           const uint32_t loc = id - qbase;
@@ -807,7 +816,7 @@ __global__ __launch_bounds__(kQBlock, 4) void k_fold_q(DecodeArgs a) {
         s_mark[q][lane] = 0u;
       }
       for (uint32_t e = st + lane; e < en; e += 64)
-        fold_q_entry(pk, w, qt, qbase, (uint32_t)base + pidx[e], pval[e]);
+        fold_q_entry<DEC>(pk, w, qt, qbase, (uint32_t)base + pidx[e], pval[e]);
     }
   } else {
     // ---- fast body: top-k / mask-selected packets; two register slots of kQGroup items, the
@@ -868,11 +877,11 @@ __global__ __launch_bounds__(kQBlock, 4) void k_fold_q(DecodeArgs a) {
           const float av = __builtin_fabsf(v);
           loc[r] = lc & (uint32_t)(kQuarter - 1);
           ok[r] = (lim > r * 64) & (!(av <= Tf) | ((av == Tf) & (lc >= Tr)));
-          tv[r] = qt[loc[r]];
+          tv[r] = DEC ? 0.f : qt[loc[r]];
         }
 #pragma unroll
         for (int r = 0; r < kQR; ++r)
-          if (ok[r]) qt[loc[r]] = __fadd_rn(tv[r], __fmul_rn(vs_[sl][d][r], w));
+          if (ok[r]) qt[loc[r]] = DEC ? vs_[sl][d][r] : __fadd_rn(tv[r], __fmul_rn(vs_[sl][d][r], w));
         if (kQTail > kQR && qn > (uint32_t)(kQR * 64)) {          // rare, uniform: the rest
           uint32_t st, en;
           range(m, st, en);
@@ -884,7 +893,7 @@ __global__ __launch_bounds__(kQBlock, 4) void k_fold_q(DecodeArgs a) {
             const float av = __builtin_fabsf(v);
             const uint32_t l2 = lc & (uint32_t)(kQuarter - 1);
             if (!(av <= Tf) | ((av == Tf) & (lc >= Tr)))
-              qt[l2] = __fadd_rn(qt[l2], __fmul_rn(v, w));
+              qt[l2] = DEC ? v : __fadd_rn(qt[l2], __fmul_rn(v, w));
           }
         }
       }
@@ -978,6 +987,7 @@ template __global__ void k_decode<FC_FMT_BITMAP, false, false>(DecodeArgs);
 template __global__ void k_decode<FC_FMT_BITMAP, false, true>(DecodeArgs);
 template __global__ void k_fold_q<false>(DecodeArgs);
 template __global__ void k_fold_q<true>(DecodeArgs);
+template __global__ void k_fold_q<false, true>(DecodeArgs);
 template __global__ void k_decode_sparse<false>(DecodeArgs);
 template __global__ void k_decode<FC_FMT_BITMAP, true, false>(DecodeArgs);
 
