@@ -714,7 +714,11 @@ __global__ __launch_bounds__(kQBlock, 4) void k_fold_q(DecodeArgs a) {
   __shared__ QMeta s_meta[kSparseMaxM];
   __shared__ uint32_t s_mark[4][kQuarter / 32];   // poisoning packets: kept-location bits
   __shared__ uint32_t s_slow;
-  const int tid = threadIdx.x, lane = lane_id(), q = tid >> 6;
+  const int tid = threadIdx.x, lane = lane_id();
+  // wave-uniform to the compiler (tid >> 6 is not): every range derived from q stays scalar and
+  // the entry loads take a scalar base + 32-bit lane offset instead of per-lane 64-bit
+  // addresses (fewer VALU per entry: the fold is issue-bound, not byte-bound)
+  const int q = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t M = (uint32_t)a.m;
   const uint32_t c = blockIdx.x;
   const uint64_t base = (uint64_t)c * kChunk;
@@ -825,9 +829,12 @@ __global__ __launch_bounds__(kQBlock, 4) void k_fold_q(DecodeArgs a) {
     // compare and comp >= T64 in float form:
     //     comp >= T64  <=>  !(|v| <= Tf)  ||  (|v| == Tf && lc >= Ti - chunk base)
     // (Tf = T64's key as a float; NaN is unordered -> kept, its key is above every finite T).
-    // Lanes past the item's end re-read its last entry and are never written; every tile read
-    // is masked into the quarter.  (Round 2's form — 64-bit comps and a branch per read —
-    // spent 34 VALU lane-ops per entry.)
+    // Lanes past the item's end re-read its last entry and fold into a dummy slot; every tile
+    // read is masked into the quarter.  (Round 2's form — 64-bit comps and a branch per read —
+    // spent 34 VALU lane-ops per entry.  A uint8-index packet, ABI 4 with 64-B segment rows,
+    // cut the packet bytes 16 % and made this fold 7-9 % SLOWER: the segment of each entry
+    // costs VALU, and the fold is issue-bound — branch exp/abi4-u8-index,
+    // profiles/r03_ab_abi4_u8_index.jsonl.)
     uint32_t ids_[2][kQGroup][kQR];
     float vs_[2][kQGroup][kQR];
     uint32_t qn_[2][kQGroup];                                   // the item's entries (uniform)
@@ -867,21 +874,24 @@ __global__ __launch_bounds__(kQBlock, 4) void k_fold_q(DecodeArgs a) {
         const uint32_t Tr = Ti <= b32 ? 0u : min(Ti - b32, (uint32_t)kChunk);   // tie cut in the chunk
         const uint32_t qn = qn_[sl][d];
         const int lim = (int)qn - lane;                           // entries left for this lane
-        uint32_t loc[kQR];
-        bool ok[kQR];
+        // branch-free: a lane whose entry is not folded (past the item's end, or slack below
+        // T64) reads and writes its own dummy slot in s_mark (used only by slow-body waves)
+        // instead of an exec-mask branch around every tile access
+        float* slot[kQR];
         float tv[kQR];
+        float* dummy = reinterpret_cast<float*>(&s_mark[q][lane]);
 #pragma unroll
         for (int r = 0; r < kQR; ++r) {                           // all tile reads, then writes
           const uint32_t lc = ids_[sl][d][r];                     // chunk-local
           const float v = vs_[sl][d][r];
           const float av = __builtin_fabsf(v);
-          loc[r] = lc & (uint32_t)(kQuarter - 1);
-          ok[r] = (lim > r * 64) & (!(av <= Tf) | ((av == Tf) & (lc >= Tr)));
-          tv[r] = DEC ? 0.f : qt[loc[r]];
+          const bool ok = (lim > r * 64) & (!(av <= Tf) | ((av == Tf) & (lc >= Tr)));
+          slot[r] = ok ? qt + (lc & (uint32_t)(kQuarter - 1)) : dummy;
+          tv[r] = DEC ? 0.f : *slot[r];
         }
 #pragma unroll
         for (int r = 0; r < kQR; ++r)
-          if (ok[r]) qt[loc[r]] = DEC ? vs_[sl][d][r] : __fadd_rn(tv[r], __fmul_rn(vs_[sl][d][r], w));
+          *slot[r] = DEC ? vs_[sl][d][r] : __fadd_rn(tv[r], __fmul_rn(vs_[sl][d][r], w));
         if (kQTail > kQR && qn > (uint32_t)(kQR * 64)) {          // rare, uniform: the rest
           uint32_t st, en;
           range(m, st, en);
