@@ -283,10 +283,18 @@ static int launch_fused(const CompactArgs& ca, const SamplePlan& P, const HdrIni
   return FC_OK;
 }
 
+// k_resolve workgroups per client: `want`, fewer for a small gradient, more when a workgroup would
+// get more than kResolveChunksMax chunks (its LDS size list; with more it reports RETRY: a lone
+// encode near n = 2^32, a batch of gradients above 128 M elements)
+static uint32_t resolve_grid(uint32_t nchunks, uint32_t want) {
+  const uint32_t g = nchunks < want ? nchunks : want;
+  const uint32_t need = (nchunks + kResolveChunksMax - 1) / kResolveChunksMax;
+  return g > need ? g : need;
+}
+
 static int launch_resolve(const ResolveArgs& a, hipStream_t s) {
   TimedLaunch t(FC_TIME_ENGINE, s);
-  const uint32_t grid = a.nchunks < (uint32_t)kResolveGrid ? a.nchunks : (uint32_t)kResolveGrid;
-  hipLaunchKernelGGL(k_resolve, dim3(grid), dim3(kBlock), 0, s, a);
+  hipLaunchKernelGGL(k_resolve, dim3(resolve_grid(a.nchunks, kResolveGrid)), dim3(kBlock), 0, s, a);
   FC_LAUNCHED("k_resolve");
   return FC_OK;
 }
@@ -513,7 +521,7 @@ int fc_topk_encode_batch_part(const fc_encode_job* jobs, int m, uint64_t n, uint
   {
     TimedLaunch t(FC_TIME_ENGINE, s);
     // fewer resolve workgroups per client than a lone encode: the batch fills the chip
-    const uint32_t rg = ca.nchunks < (uint32_t)kResolveGridBatch ? ca.nchunks : (uint32_t)kResolveGridBatch;
+    const uint32_t rg = resolve_grid(ca.nchunks, kResolveGridBatch);
     hipLaunchKernelGGL(k_resolve, dim3(rg, (uint32_t)m), dim3(kBlock), 0, s, ra);
     FC_LAUNCHED("k_resolve(batch)");
   }

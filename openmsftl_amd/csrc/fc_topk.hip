@@ -991,7 +991,7 @@ template __global__ void k_fused_mag<true>(CompactArgs, SamplePlan, HdrInit, uin
 // entry is a candidate of its chunk, so the workgroups that gathered a chunk range wait for the
 // last one to publish T64 (generation counter, release/acquire) and zero the slack of their
 // own range: no fix-up launch (it took 13.8 us per 128 M gradient as its own kernel).  The
-// wait is safe: the grid (<= 256 workgroups, 3 per CU by LDS) is always co-resident, and the
+// wait is safe: the grid (<= 512 workgroups, 4 per CU by LDS) is always co-resident, and the
 // spin is bounded (FC_STATUS_TIMEOUT, never expected).
 // --------------------------------------------------------------------------------------
 struct ResolveArgs {
@@ -1011,7 +1011,10 @@ struct ResolveArgs {
                                // unfused and rand-k); 0: k_fused_mag filled the histogram
 };
 
-constexpr int kResolveChunksMax = 2048;   // chunks per workgroup handled through LDS sizes
+// chunks per workgroup (their gather sizes live in LDS; the launches size the grid so that no
+// workgroup gets more).  1024 keeps the workgroup at 36.9 KB of LDS = 4 per CU: at 2048 (41 KB,
+// 3 per CU) a 64-client batch's 1024 workgroups did not fit one round.
+constexpr int kResolveChunksMax = 1024;
 
 __global__ __launch_bounds__(kBlock) void k_resolve(ResolveArgs a0) {
   ResolveArgs a = a0;

@@ -392,6 +392,37 @@ def test_batch_encode_parts_more_groups_than_streams():
     assert [_packet_bytes(p) for p in pk] == want
 
 
+def test_batch_encode_above_resolve_chunk_list():
+    """n = 2^28 + 8193 (32,769 chunks): 16 resolve workgroups per client would each own more
+    chunks than the k_resolve LDS size list holds (the call came back RETRY for every client
+    and went down the exact path); the launch adds workgroups instead.  Straight out of the
+    batch launch every status is OK and the packets equal the lone encodes'."""
+    codec = _codec()
+    n, M = (1 << 28) + 8193, 2
+    grads = [torch.randn(n, device="cuda", generator=torch.Generator(device="cuda").manual_seed(s))
+             .mul_(10.0 ** -s) for s in range(M)]
+    k = co.num_kept(0.1, n)
+    from openmsftl_amd import _lib as L
+    pk = codec.encode_top_batch(grads, k, check=False)
+    torch.cuda.synchronize()
+    assert [int(h.status) for h in codec.headers(pk)] == [0] * M
+    for g, pb in zip(grads, pk):
+        ps = codec.encode_top(g, k, check=False)
+        hb, hs = codec.headers([pb, ps])
+        assert int(hs.status) == 0
+        assert (hb.thresh, hb.lower, hb.n_entries) == (hs.thresh, hs.lower, hs.n_entries)
+        assert torch.equal(pb.cnt, ps.cnt) and torch.equal(pb.qoff, ps.qoff)
+        pos = torch.arange(pb.capacity, device="cuda")       # the listed slot entries, on the GPU
+        listed = (pos % L.FC_CHUNK) < pb.cnt.long()[pos // L.FC_CHUNK]
+        del pos
+        assert int(listed.sum()) == int(hb.n_entries)
+        assert torch.equal(pb.idx[listed], ps.idx[listed])
+        assert torch.equal(pb.val.view(torch.int32)[listed], ps.val.view(torch.int32)[listed])
+        del ps, listed
+    del pk, grads
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("M,n", [(65, 20_000), (70, 8_193 * 3), (130, 9_000)])
 def test_batch_encode_client_interleave(M, n):
     """k_compact_mag1 interleaves the chunks of 64 clients in dispatch order: a full group, a
