@@ -522,7 +522,7 @@ def single_gradient(torch, codec, g, k, n, iters=20):
                             "hbm_frac": round(alg / dt_d / 1e9 / HBM_PEAK_GBPS, 4)}}
 
 
-def small_configs(torch, codec, L, device, f, n=16_777_216, M=128, steps=20):
+def small_configs(torch, codec, L, device, f, n=16_777_216, M=128, steps=100):
     """BASELINE configs[1] (one 16 M gradient: encode + dense decode) and configs[2] (128
     clients x 16 M: batched encode + on-device FedAVG fold), device-resident, same codec."""
     from openmsftl_amd.compression import kept_count
@@ -539,7 +539,7 @@ def small_configs(torch, codec, L, device, f, n=16_777_216, M=128, steps=20):
         codec.encode_top_batch(grads, k, packets=pkts, jobs=jobs, check=False)
         codec.decode_accumulate(pkts, w, out=acc, views=views)
 
-    for _ in range(2):
+    for _ in range(10):                 # 2.4 ms steps: warm enough that clocks have settled
         step()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
