@@ -72,11 +72,12 @@ def parse():
     return ap.parse_args()
 
 
-def spawn_ranks(argv, nproc):
+def spawn_ranks(argv, nproc, script=None):
     """`bench.py --gpus N` without a launcher: start N ranks (one process per GPU, the env
     torch.distributed.run would set: RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*) as CHILD
-    processes, before this process touches the GPU, and return the worst exit code (never
-    exec: the parent stays alive and GPU-free).  A rank that fails ends the others."""
+    processes running ``script`` (default this file), before this process touches the GPU, and
+    return the worst exit code (never exec: the parent stays alive and GPU-free).  A rank that
+    fails ends the others."""
     import socket
     import subprocess
     with socket.socket() as s:
@@ -86,8 +87,8 @@ def spawn_ranks(argv, nproc):
     for r in range(nproc):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nproc),
                    LOCAL_WORLD_SIZE=str(nproc), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv),
-                                      env=env))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(script or __file__)]
+                                      + list(argv), env=env))
     log(f"[launcher] {nproc} ranks, pids {[p.pid for p in procs]}, port {port}")
     rc = 0
     live = list(procs)

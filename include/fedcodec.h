@@ -37,7 +37,11 @@ extern "C" {
 
 typedef void* fc_stream_t; /* hipStream_t */
 
-#define FC_ABI_VERSION 3
+/* ABI history: 2 = per-chunk quarter offsets (qoff); 3 = uint16 chunk-local packet indices;
+ * 4 = fc_topk_encode_dense's packet is scratch (no entries; header format FC_FMT_DENSE, which
+ * the decode entry points must not be given: they trust the caller's format argument).  A C
+ * caller built against 3 that decoded that packet must check this version. */
+#define FC_ABI_VERSION 4
 
 /* return codes */
 #define FC_OK 0
@@ -279,7 +283,17 @@ int fc_qsgd_decode_accumulate(const fc_packet_view* views_dev, int m, uint64_t n
  *   array of m row pointers (float32 if rows_f64 == 0, promoted exactly), w = DEVICE
  *   float64[m]; out = +0-started row-order fp64 sum of fl64(g_i * w_i); continue_sum != 0
  *   continues the sum already in out.
- * fc_div_scalar_f64: x = fl64(x / d) in place (np.mean's count division for float64 G). */
+ * fc_div_scalar_f64: x = fl64(x / d) in place (np.mean's count division for float64 G).
+ * fc_topk_dense_f64_sampled: 'top' (magnitude keys, 0 < k < n, g / out 16-B aligned) by the
+ *   fp32 design on each double's high 31-bit key: sampled bracket, ONE streaming pass that
+ *   writes out and lists the bracket's candidates, exact select among them, slack fix-up
+ *   (replaces compression.py:31-37 for float64 client.grad; 8N read + 8N written instead of
+ *   <= 8 passes of 8N).  Writes *status (DEVICE uint32) = FC_STATUS_OK, or
+ *   FC_STATUS_RETRY_EXACT when the bracket missed / a chunk's candidate slot overflowed: out
+ *   is then not valid and the caller runs fc_topk_dense_f64 (exact).  Same result bits as
+ *   fc_topk_dense_f64.  ws: fc_workspace_bytes(n), zeroed once. */
+int fc_topk_dense_f64_sampled(const double* g, uint64_t n, uint64_t k, double* out, void* ws,
+                              size_t ws_bytes, uint32_t* status, fc_stream_t stream);
 int fc_topk_dense_f64(const double* g, uint64_t n, uint64_t k, int key_mode, uint64_t seed,
                       uint64_t offset, double* out, void* ws, size_t ws_bytes,
                       fc_stream_t stream);

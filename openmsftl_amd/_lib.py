@@ -96,6 +96,7 @@ SIGNATURES = {
     "fc_qsgd_decode": (_i32, [ctypes.POINTER(PacketView), _u64, _vp, _vp]),
     "fc_qsgd_decode_accumulate": (_i32, [_vp, _i32, _u64, _vp, _i32, _vp]),
     "fc_topk_dense_f64": (_i32, [_vp, _u64, _u64, _i32, _u64, _u64, _vp, _vp, _sz, _vp]),
+    "fc_topk_dense_f64_sampled": (_i32, [_vp, _u64, _u64, _vp, _vp, _sz, _vp, _vp]),
     "fc_mask_dense_f64": (_i32, [_vp, _u64, _i32, _vp, _dbl, _u64, _u64, _vp, _vp]),
     "fc_mask_dense_f32": (_i32, [_vp, _u64, _i32, _vp, _dbl, _u64, _u64, _vp, _vp]),
     "fc_weighted_sum_dense_f64": (_i32, [_vp, _i32, _vp, _i32, _u64, _vp, _i32, _vp]),
@@ -159,7 +160,9 @@ def load(path: str = LIB_PATH):
                 continue                        # an older A/B build (tools/ab.py --lib)
             fn.restype = res
             fn.argtypes = args
-        if lib.fc_abi_version() != 3:
+        # the product library is ABI 4; an A/B build (tools/ab.py --lib) may predate the bump
+        # (3 differs only in the documented fc_topk_encode_dense packet contract)
+        if lib.fc_abi_version() not in ((4,) if path == LIB_PATH else (3, 4)):
             raise FedCodecUnavailable("libfedcodec.so ABI mismatch")
         _lib = lib
         return lib

@@ -5,11 +5,14 @@ The reference builds the dense host matrix ``G`` (M x N) row by row from
 (``__merge_gradient``, aggregation.py:80-93, ``num_hierarchies > 0``) and reduces it with the
 GAR (gar.py:44).  Here the rows never become a dense matrix on the common path:
 
-* every client's gradient goes to the GPU once; when all clients compress with ``'top'`` at
-  one fraction (the configured codec, client_config.json:48-50) they are encoded in ONE
-  batched launch sequence (``fc_topk_encode_batch``) into device packets;
-* without hierarchies the packets are folded straight into the FedAVG sum
-  (``fc_decode_accumulate``: bit-exact ``np.sum(G * w[:, None], axis=0)``);
+* when all clients compress with ``'top'`` at one fraction (the configured codec,
+  client_config.json:48-50) their host gradients stream through a bounded device ring
+  (openmsftl_amd/pipeline.py): H2D, ``fc_topk_encode`` into packets, and every group of
+  packets folded into the FedAVG sum (``fc_decode_accumulate``: bit-exact
+  ``np.sum(G * w[:, None], axis=0)``).  On a node with several GPUs the groups go
+  round-robin to one pipeline per GPU, driven by one host thread each, and the running sum
+  hops between the GPUs in group order (``aggregation_config["devices"]``, default every
+  visible GPU: the reference's single-process server loop, server.py:98-100, drives them all);
 * with hierarchies each first-stage cluster mean is the packet fold with weights 1 (the
   +0-started row-order sum ``np.mean`` computes) divided once by the row count
   (``fc_div_scalar``); later stages do the same over the dense merged rows
@@ -36,9 +39,11 @@ from typing import Dict, List, Optional
 import numpy as np
 import torch
 
+from . import _lib as L
 from . import codec
 from .compression import Compression, kept_count
 from .gar import FedAvg
+from .pipeline import HostFedAvg
 
 
 def _cluster_bounds(m: int, cluster_size: int):
@@ -56,6 +61,40 @@ def _device_of(agg) -> torch.device:
     if isinstance(dev, torch.device) and dev.type == "cuda":
         return dev
     return torch.device("cuda", torch.cuda.current_device())
+
+
+#: default for aggregation_config["devices"] (``integration.install(devices=...)`` sets it):
+#: "all" = every visible GPU of this process drives the streamed top-k path
+DEFAULT_DEVICES = "all"
+
+
+def stream_devices(agg) -> List[torch.device]:
+    """The GPUs the streamed top-k path fans out over (one process, one pipeline each):
+    ``aggregation_config["devices"]`` = "all" (every visible GPU), a count (the first n) or a
+    list of device indices (repeats allowed: tests stand two pipelines on one GPU in for two
+    GPUs); absent -> :data:`DEFAULT_DEVICES`.  An aggregator constructed with an explicit
+    ``device`` and no ``devices`` key stays on that device."""
+    cfg = getattr(agg, "aggregation_config", None) or {}
+    spec = cfg.get("devices")
+    if spec is None:
+        if isinstance(getattr(agg, "device", None), torch.device):
+            return [_device_of(agg)]
+        spec = DEFAULT_DEVICES
+    if spec is None or spec == 1:
+        return [_device_of(agg)]
+    if spec == "all":
+        count = torch.cuda.device_count()
+        if count <= 1:
+            return [_device_of(agg)]
+        return [torch.device("cuda", i) for i in range(count)]
+    if isinstance(spec, int):
+        if not 1 <= spec <= torch.cuda.device_count():
+            raise ValueError(f"devices={spec}: {torch.cuda.device_count()} visible GPU(s)")
+        return [torch.device("cuda", i) for i in range(spec)]
+    devs = [torch.device("cuda", int(i)) for i in spec]
+    if not devs:
+        raise ValueError("devices: empty list")
+    return devs
 
 
 def common_top_fraction(clients) -> Optional[float]:
@@ -88,17 +127,24 @@ def _budget(agg, dev: torch.device) -> int:
     return int(free * DEFAULT_BUDGET_FRACTION)
 
 
-def _stream_pipeline(agg, n: int, k: int, m: int, dev: torch.device):
-    """The aggregator's cached HostFedAvg for (n, k), its fold group sized for the budget."""
-    from .pipeline import HostFedAvg, plan_group
+def _stream_pipeline(agg, n: int, k: int, m: int, devs: List[torch.device]):
+    """The aggregator's cached streaming pipeline for (n, k) on ``devs``: one HostFedAvg, or
+    a DeviceRing of one HostFedAvg (two packet sets) per device; fold groups sized for the
+    per-device budget."""
+    from .pipeline import DeviceRing, HostFedAvg, plan_group
     cache = agg.__dict__.setdefault("_host_pipelines", {})
-    group = plan_group(n, m, _budget(agg, dev))
-    key = (n, k, dev.index)
+    sets = 1 if len(devs) == 1 else 2
+    group = min(plan_group(n, m, _budget(agg, d), sets=sets) for d in devs)
+    key = (n, k, tuple(d.index for d in devs))
     pipe = cache.get(key)
     if pipe is None or pipe.group < group:
         cache.clear()                       # one shape at a time: release the old buffers
         torch.cuda.empty_cache()
-        pipe = cache[key] = HostFedAvg(n, k, group=group, device=dev)
+        if len(devs) == 1:
+            pipe = HostFedAvg(n, k, group=group, device=devs[0])
+        else:
+            pipe = DeviceRing([HostFedAvg(n, k, group=group, device=d, sets=2) for d in devs])
+        cache[key] = pipe
     return pipe
 
 
@@ -107,19 +153,33 @@ def stream_top_fold(agg, clients, n: int, f: float, weights: np.ndarray, dev: to
     """FedAVG of the clients' top-k rows (aggregation.py:61-63 + gar.py:44) streamed from
     their host ``client.grad`` through a bounded H2D ring, encoded and folded group by group
     (openmsftl_amd/pipeline.py): device memory stays within the budget for any client count.
-    Returns the device aggregate (``out`` if given)."""
+    With several devices (:func:`stream_devices`) the groups go round-robin to one pipeline
+    per GPU and the running aggregate hops between them in group order (pipeline.DeviceRing):
+    the same bits, every GPU's PCIe link busy.  Returns the device aggregate (``out`` if
+    given, else on the device that folded the last group)."""
     k = kept_count(f, n)
-    if not 0 < k < n:                       # trivial k (0, all): one packet per client, no ring
-        w = [float(x) for x in weights]
-        acc = out
-        for g0 in range(0, len(clients), 64):
-            sub = clients[g0:g0 + 64]
-            pk = [codec.encode_top(torch.from_numpy(np.ascontiguousarray(c.grad)).to(dev), k)
-                  for c in sub]
-            acc = codec.decode_accumulate(pk, w[g0:g0 + len(sub)], out=acc, continue_sum=g0 > 0)
+    w = np.asarray(weights, np.float32)
+    if not 0 < k < n:
+        # trivial k (0, all rows): the exact engine, one client at a time through one device
+        # slot and one packet, so the device bytes stay bounded whatever the client count
+        slot = torch.empty(n, dtype=torch.float32, device=dev)
+        pkt = codec.Packet.alloc(n, L.FC_FMT_IDXVAL, dev, k=k)
+        acc = out if out is not None else torch.empty(n, dtype=torch.float32, device=dev)
+        for i, c in enumerate(clients):
+            slot.copy_(torch.from_numpy(np.ascontiguousarray(c.grad)))
+            codec.encode_top(slot, k, packet=pkt)
+            codec.decode_accumulate([pkt], [float(w[i])], out=acc, continue_sum=i > 0)
         return acc
-    pipe = _stream_pipeline(agg, n, k, len(clients), dev)
-    return pipe.run(lambda i: clients[i].grad, len(clients), weights, out=out, to_host=False)
+    devs = stream_devices(agg)
+    pipe = _stream_pipeline(agg, n, k, len(clients), devs)
+    get = lambda i: clients[i].grad         # noqa: E731
+    if isinstance(pipe, HostFedAvg) and (out is None or out.device == pipe.dev):
+        return pipe.run(get, len(clients), w, out=out, to_host=False)
+    acc = pipe.run(get, len(clients), w, to_host=False)
+    if out is None:
+        return acc
+    out.copy_(acc)
+    return out
 
 
 def merge_streamed(agg, clients, n: int, f: float, cluster_size: int,

@@ -247,6 +247,11 @@ class BatchWorkspace:
 
 _SIDE: dict = {}
 _MAX_SIDE = 4          # GPU_MAX_HW_QUEUES is 4: more forked streams would share queues
+# Above 2^27 elements per client a batched k_resolve gives each client more than
+# kResolveGridBatch (16) workgroups, up to 512, which wait for each other in-kernel: such
+# batches run on one stream, where at most one client is ever partly dispatched
+# (fc_topk.hip, k_resolve's residency note).  Packets are identical either way.
+_ONE_STREAM_N = 1 << 27
 
 
 def _side_streams(dev: torch.device, count: int = 2) -> list:
@@ -297,7 +302,12 @@ def encode_top_batch(grads: Sequence[torch.Tensor], k: int, *,
     n, dev = grads[0].numel(), grads[0].device
     # per-tensor checks once per (jobs table, gradient / packet set): a 128-client step spent
     # ~1 ms of host time in them, which shows as GPU idle time when a step is short (16 M)
-    key = (n, tuple(map(id, grads)), tuple(map(id, packets)) if packets is not None else None)
+    # keyed on what the checks depend on (buffer address, length, dtype, device of every
+    # tensor), not on id(): CPython reuses ids of collected objects
+    sig = lambda t: (t.data_ptr(), t.numel(), t.dtype, t.device)          # noqa: E731
+    key = (n, tuple(sig(g) for g in grads),
+           tuple((sig(p.val), sig(p.idx), sig(p.cnt), sig(p.hdr), p.fmt, p.capacity)
+                 for p in packets) if packets is not None else None)
     checked = jobs is not None and getattr(jobs, "_fc_checked", None) == key
     if not checked:
         for g in grads:
@@ -330,6 +340,8 @@ def encode_top_batch(grads: Sequence[torch.Tensor], k: int, *,
     elif not checked:
         jobs._fc_checked = key
     nside = max(1, min(int(streams), m, _MAX_SIDE))
+    if n > _ONE_STREAM_N:
+        nside = 1
     if groups is None:
         groups = [(i + 1) * m // nside - i * m // nside for i in range(nside)]
     groups = [int(x) for x in groups]
@@ -401,6 +413,8 @@ def encode_fold_batch(grads: Sequence[torch.Tensor], k: int, weights, out: torch
     if views is None:
         views = views_tensor(packets, weights, dev)
     nside = max(1, min(int(streams), m, _MAX_SIDE))
+    if n > _ONE_STREAM_N:
+        nside = 1                                   # (k_resolve residency, see encode_top_batch)
     groups = [(i + 1) * m // nside - i * m // nside for i in range(nside)]
     jb, vb = ctypes.sizeof(L.EncodeJob), ctypes.sizeof(L.PacketView)
     main = torch.cuda.current_stream(dev)
@@ -600,11 +614,28 @@ def div_scalar(x: torch.Tensor, d: float) -> torch.Tensor:
 
 
 # ---- float64 gradients (attack_models.py:105-106 -> aggregation.py:61) ----------------------
+_F64_STATUS: dict = {}
+
+
+def _f64_status(device: torch.device) -> torch.Tensor:
+    key = (device.index if device.index is not None else torch.cuda.current_device(),
+           torch.cuda.current_stream(device).cuda_stream)
+    st = _F64_STATUS.get(key)
+    if st is None:
+        st = _F64_STATUS[key] = torch.zeros(1, dtype=_U32, device=device)
+    return st
+
+
 def compress_top_dense_f64(g: torch.Tensor, k: int, *, key_mode: int = L.FC_KEY_MAGNITUDE,
                            seed: int = 0, offset: int = 0,
-                           out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                           out: Optional[torch.Tensor] = None, check: bool = True,
+                           exact: bool = False) -> torch.Tensor:
     """compression.py:31-37 ('top') / native 'rand' (PHILOX keys) on a float64 gradient: the
-    dense float64 q (fc_topk_dense_f64, exact radix select; same tie rule as fp32)."""
+    dense float64 q (same tie rule as fp32).  'top' with 0 < k < n takes the sampled path
+    (fc_topk_dense_f64_sampled: one streaming pass); ``check=True`` reads its status (one
+    sync) and re-runs a missed bracket exactly; with ``check=False`` call
+    :func:`resolve_f64` after the last call on this stream.  Native rand-k, trivial k and
+    ``exact=True``: the exact radix select (fc_topk_dense_f64)."""
     _require_cuda_f32(g, align=8, dtype=torch.float64)
     n = g.numel()
     if not 0 <= k <= n:
@@ -612,11 +643,35 @@ def compress_top_dense_f64(g: torch.Tensor, k: int, *, key_mode: int = L.FC_KEY_
     if out is None:
         out = torch.empty(n, dtype=torch.float64, device=g.device)
     _require_cuda_f32(out, "out", align=8, dtype=torch.float64)
+    if out.numel() != n:
+        raise ValueError("out must have n elements")
     lib = L.load()
     ws = Workspace.get(n, g.device)
+    sampled = (not exact and key_mode == L.FC_KEY_MAGNITUDE and 0 < k < n
+               and g.data_ptr() % 16 == 0 and out.data_ptr() % 16 == 0)
+    if sampled:
+        st = _f64_status(g.device)
+        L.check(lib.fc_topk_dense_f64_sampled(_vp(g), n, k, _vp(out), _vp(ws.buf), ws.nbytes,
+                                              _vp(st), _stream(g.device)),
+                "fc_topk_dense_f64_sampled")
+        out._fc_f64_enc = (g, k)
+        if check:
+            resolve_f64(out)
+        return out
     L.check(lib.fc_topk_dense_f64(_vp(g), n, k, key_mode, seed, offset, _vp(out), _vp(ws.buf),
                                   ws.nbytes, _stream(g.device)), "fc_topk_dense_f64")
     return out
+
+
+def resolve_f64(out: torch.Tensor) -> int:
+    """After sampled fp64 encodes on the current stream: if the LAST one's bracket missed
+    (its status word), redo it exactly into ``out``.  Returns 1 if it did, else 0."""
+    st = _f64_status(out.device)
+    if int(st.item()) == L.FC_STATUS_OK:
+        return 0
+    g, k = out._fc_f64_enc
+    compress_top_dense_f64(g, k, out=out, exact=True)
+    return 1
 
 
 def mask_dense_f64(g: torch.Tensor, codec: int, *, p: float = 0.5,

@@ -60,12 +60,17 @@ static WsPtrs ws_ptrs(void* ws, uint64_t n) {
 // Stratified sample + bracket ranks.  Full sample for n <= 1 M (exact bracket); otherwise
 // 64..1024 segments of 1024 (n/64 .. 1 M keys) and a +-6 sigma binomial margin.
 // Decode grid: per_cu workgroups per CU (capped at one per chunk), each walking
-// ceil(chunks / grid) chunks.  FC_DECODE_GRID overrides (tuning only).
+// ceil(chunks / grid) chunks.  FC_DECODE_GRID overrides it in FC_DEBUG_BUILD libraries only
+// (tuning); the shipped library's geometry never depends on the host environment.
 static uint32_t decode_grid(uint64_t n, uint32_t per_cu = kDecBlocksPerCU) {
+#ifdef FC_DEBUG_BUILD
   static const uint32_t forced = [] {
     const char* e = getenv("FC_DECODE_GRID");
     return e ? (uint32_t)atoi(e) : 0u;
   }();
+#else
+  constexpr uint32_t forced = 0;
+#endif
   uint32_t g = forced ? forced : 256u * per_cu;
   const uint32_t nch = num_chunks(n);
   return g < nch ? g : nch;
@@ -88,6 +93,9 @@ static uint32_t decode_grid(uint64_t n, uint32_t per_cu = kDecBlocksPerCU) {
 #endif
 #ifndef FC_MAX_SAMPLE_SEGS_SINGLE
 #define FC_MAX_SAMPLE_SEGS_SINGLE 2048
+#endif
+#ifndef FC_SAMPLE_ROUNDS
+#define FC_SAMPLE_ROUNDS 4                        // sample groups per batched k_sample1 workgroup
 #endif
 static SamplePlan make_plan(uint64_t n, uint64_t k, bool single = false) {
   SamplePlan P;
@@ -264,13 +272,17 @@ static int launch_setup(uint64_t n, uint64_t k, const WsPtrs& W, fc_packet_hdr* 
 }
 
 // k_fused_mag (sample + compaction in one launch) for a lone magnitude-key client;
-// FC_UNFUSED=1 selects the two-launch form (A/B only).
+// FC_UNFUSED=1 selects the two-launch form in FC_DEBUG_BUILD libraries only (A/B).
 static bool fused_enabled() {
+#ifdef FC_DEBUG_BUILD
   static const bool on = [] {
     const char* e = getenv("FC_UNFUSED");
     return !(e && atoi(e) != 0);
   }();
   return on;
+#else
+  return true;
+#endif
 }
 
 static int launch_fused(const CompactArgs& ca, const SamplePlan& P, const HdrInit& hi,
@@ -506,7 +518,8 @@ int fc_topk_encode_batch_part(const fc_encode_job* jobs, int m, uint64_t n, uint
   ra.rbin = 1;                       // batched compaction: k_resolve bins the candidates
   hipStream_t s = (hipStream_t)stream;
   const SamplePlan P = make_plan(n, k);
-  const dim3 sgrid((P.nseg + kSampleSegs - 1) / kSampleSegs, (uint32_t)m);
+  // FC_SAMPLE_ROUNDS sample groups per workgroup (k_sample1): the same sample, fewer workgroups
+  const dim3 sgrid((P.pstride + FC_SAMPLE_ROUNDS - 1) / FC_SAMPLE_ROUNDS, (uint32_t)m);
   if (part & FC_PART_SAMPLE) {
     int rc = key_mode == FC_KEY_PHILOX
                  ? launch_setup(n, k, ca.W, nullptr, hi, jobs, stride, (uint32_t)m, s)
@@ -777,6 +790,56 @@ static uint32_t grid_of(uint64_t n) {
   if (b < 1) b = 1;
   if (b > 2048) b = 2048;
   return (uint32_t)b;
+}
+
+int fc_topk_dense_f64_sampled(const double* g, uint64_t n, uint64_t k, double* out, void* ws,
+                              size_t ws_bytes, uint32_t* status, fc_stream_t stream) {
+  FC_CHECK(g && out && ws && status, "NULL argument");
+  FC_CHECK(n >= 2 && n <= 0xffffffffull, "n=%llu outside [2, 2^32-1]", (unsigned long long)n);
+  FC_CHECK(k > 0 && k < n, "the sampled fp64 path needs 0 < k < n (k=%llu, n=%llu)",
+           (unsigned long long)k, (unsigned long long)n);
+  FC_CHECK(((uintptr_t)g & 15) == 0 && ((uintptr_t)out & 15) == 0, "g and out must be 16-B aligned");
+  const WsLayout Lw = WsLayout::of(n);
+  if (ws_bytes < Lw.bytes)
+    return fail(FC_ERR_WORKSPACE, "workspace %zu B < %llu B needed", ws_bytes,
+                (unsigned long long)Lw.bytes);
+  const WsPtrs W = ws_ptrs(ws, n);
+  hipStream_t s = (hipStream_t)stream;
+  const SamplePlan P = make_plan(n, k, true);
+  const uint32_t ib = index_bits(n);
+  HdrInit hi;
+  memset(&hi, 0, sizeof hi);
+  hi.n = (uint32_t)n; hi.k = (uint32_t)k; hi.ib = ib; hi.codec = FC_CODEC_TOP;
+  hi.format = FC_FMT_DENSE; hi.key_mode = FC_KEY_MAGNITUDE;
+  auto* hdr = reinterpret_cast<fc_packet_hdr*>(static_cast<char*>(ws) + kHdr64Off);
+  Fast64Args a;
+  memset(&a, 0, sizeof a);
+  a.g = g; a.n = n; a.k = k; a.nchunks = (uint32_t)Lw.nchunks;
+  a.per = 16;                                    // chunks per resolve / fix-up workgroup
+  a.S = W.st; a.E = reinterpret_cast<Eng64State*>(static_cast<char*>(ws) + kEng64Off);
+  a.ccnt = W.ccnt; a.cand = reinterpret_cast<u128*>(W.cand); a.chist = W.chist;
+  a.tick = W.tick + 2 * kTickWords; a.small = reinterpret_cast<u128*>(W.small);
+  a.out = out; a.status = status;
+  const uint32_t rgrid = (a.nchunks + a.per - 1) / a.per;
+  {
+    TimedLaunch t(FC_TIME_SAMPLE, s);
+    hipLaunchKernelGGL(k_sample64, dim3((P.nseg + kSampleSegs - 1) / kSampleSegs), dim3(kBlock),
+                       0, s, g, P, W, ib, hdr, hi);
+    FC_LAUNCHED("k_sample64");
+  }
+  {
+    TimedLaunch t(FC_TIME_COMPACT, s);
+    hipLaunchKernelGGL(k_compact64, dim3(a.nchunks), dim3(kBlock), 0, s, a);
+    FC_LAUNCHED("k_compact64");
+  }
+  {
+    TimedLaunch t(FC_TIME_ENGINE, s);
+    hipLaunchKernelGGL(k_resolve64, dim3(rgrid), dim3(kBlock), 0, s, a);
+    FC_LAUNCHED("k_resolve64");
+    hipLaunchKernelGGL(k_fixup64, dim3(rgrid), dim3(kBlock), 0, s, a);
+    FC_LAUNCHED("k_fixup64");
+  }
+  return FC_OK;
 }
 
 int fc_topk_dense_f64(const double* g, uint64_t n, uint64_t k, int key_mode, uint64_t seed,

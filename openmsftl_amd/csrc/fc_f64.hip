@@ -289,6 +289,235 @@ __global__ __launch_bounds__(kBlock) void k_div_scalar64(double* x, uint64_t n, 
     x[e] = __ddiv_rn(x[e], d);
 }
 
+// --------------------------------------------------------------------------------------
+// Sampled fast path for magnitude keys (fc_topk_dense_f64_sampled): the fp32 design on the
+// 31-bit HIGH key hk(x) = (|x| bits) >> 32 of each double (exponent + 20 mantissa bits;
+// key32 = mag_key of it, a non-decreasing map of the 95-bit comp = key64 << 32 | idx):
+//   k_sample64    k_sample1's stratified sample + pilot window over hk (sample_body<double>):
+//                 bracket [t_lo, t_hi] of key32 around the k-th key (one launch)
+//   k_compact64   ONE streaming pass, 8N read + 8N written: q = key32 >= t_lo ? g : +0;
+//                 definite (key32 > t_hi) and candidate counts into the sharded totals; each
+//                 candidate's exact comp into its chunk's slot, its bin into the histogram
+//   k_resolve64   rank r = k - #definite among the candidates: every workgroup finds the bin
+//                 beta holding it (the histogram, from L2) and gathers its chunks' candidates
+//                 in beta; the last arriver sorts them (<= 2048, LDS) and picks T, the exact
+//                 k-th largest comp; any miss (bracket, slot overflow, big bin) -> RETRY
+//   k_fixup64     q[idx] = +0 for every candidate with comp < T
+// The exact radix engine (<= 8 passes of 8N) stays the fallback and serves native rand-k.
+// --------------------------------------------------------------------------------------
+constexpr int kC64Slot = 128;                  // candidate comps per chunk (the 2 KB slot)
+constexpr uint64_t kHdr64Off = 896;            // the sample's scratch packet header
+static_assert(kEng64Off + sizeof(Eng64State) <= kHdr64Off && kHdr64Off + sizeof(fc_packet_hdr) <= 1024,
+              "state block layout");
+static_assert(kC64Slot * sizeof(u128) == kCandSlot * sizeof(uint64_t), "candidate slot bytes");
+
+__device__ __forceinline__ uint32_t key32_of(double x) { return mag_key(hikey_f(x)); }
+
+__global__ __launch_bounds__(kBlock, 8) void k_sample64(const double* __restrict__ g, SamplePlan P,
+                                                     WsPtrs W, uint32_t ib, fc_packet_hdr* hdr,
+                                                     HdrInit HI) {
+  __shared__ SampleShared sm;
+  sample_body<kKeyMag, false, double>(g, P, 0ull, 0ull, W, ib, hdr, HI, blockIdx.x, gridDim.x,
+                                      true, sm, 0u);
+}
+
+struct Fast64Args {
+  const double* g;
+  uint64_t n, k;
+  uint32_t nchunks, per;       // per: chunks per k_resolve64 / k_fixup64 workgroup
+  TopkState* S;
+  Eng64State* E;
+  uint32_t* ccnt;              // candidates per chunk (may exceed kC64Slot: overflowed)
+  u128* cand;                  // chunk c's candidate comps at [c * kC64Slot, ...)
+  uint32_t* chist;             // 4096-bin candidate histogram (zero between calls)
+  uint32_t* tick;              // two-level ticket (k_resolve64)
+  u128* small;                 // bin beta's candidates (<= kSmallCap64)
+  double* out;
+  uint32_t* status;            // caller's device word: FC_STATUS_OK / RETRY_EXACT
+};
+
+typedef double fc_d2v __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(1))) const fc_d2v fc_gd2v;
+
+// One workgroup per 8192-element chunk: 16 double2 per thread, coalesced (element
+// base + 2 (i * 256 + tid) + {0, 1}).
+__global__ __launch_bounds__(kBlock) void k_compact64(Fast64Args a) {
+  __shared__ uint32_t s_cnt, s_red[kBlock / 64];
+  const uint32_t chunk = blockIdx.x, tid = threadIdx.x;
+  const uint64_t base = (uint64_t)chunk * kChunk;
+  const bool full = base + kChunk <= a.n;
+  constexpr int kI = kChunk / (2 * kBlock);     // 16
+  fc_d2v x[kI];
+  if (full) {
+    fc_gd2v* gp = (fc_gd2v*)(a.g + base) + tid;
+#pragma unroll
+    for (int i = 0; i < kI; ++i) x[i] = __builtin_nontemporal_load(gp + i * kBlock);
+  } else {
+#pragma unroll
+    for (int i = 0; i < kI; ++i) {
+      const uint64_t e = base + 2ull * (i * kBlock + tid);
+      x[i].x = e < a.n ? a.g[e] : 0.0;
+      x[i].y = e + 1 < a.n ? a.g[e + 1] : 0.0;
+    }
+  }
+  if (tid == 0) s_cnt = 0;
+  const uint32_t t_lo = a.S->t_lo, t_hi = a.S->t_hi, sbin = a.S->sbin;
+  lds_barrier();
+  uint32_t listed = 0;
+#pragma unroll
+  for (int i = 0; i < kI; ++i) {
+    fc_d2v q;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint64_t e = base + 2ull * (i * kBlock + tid) + h;
+      const double v = h ? x[i].y : x[i].x;
+      const uint32_t key = key32_of(v);
+      const bool L = e < a.n && key >= t_lo;
+      listed += L ? 1u : 0u;
+      if (h) q.y = L ? v : 0.0; else q.x = L ? v : 0.0;
+      if (L && key <= t_hi) {
+        const uint32_t pos = atomicAdd(&s_cnt, 1u);
+        if (pos < (uint32_t)kC64Slot) {
+          const uint64_t key64 = mag_key64(v);
+          uint64_t* d = reinterpret_cast<uint64_t*>(&a.cand[(uint64_t)chunk * kC64Slot + pos]);
+          d[0] = (key64 << 32) | (uint32_t)e;
+          d[1] = key64 >> 32;
+        }
+        atomicAdd(&a.chist[(key - t_lo) >> sbin], 1u);
+      }
+    }
+    if (full) {
+      __builtin_nontemporal_store(q, (fc_d2v*)(a.out + base) + tid + i * kBlock);
+    } else {
+      const uint64_t e = base + 2ull * (i * kBlock + tid);
+      if (e < a.n) a.out[e] = q.x;
+      if (e + 1 < a.n) a.out[e + 1] = q.y;
+    }
+  }
+  listed = wave_sum(listed);
+  if ((tid & 63) == 0) s_red[tid >> 6] = listed;
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t tot = 0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) tot += s_red[w];
+    a.ccnt[chunk] = s_cnt;
+    atomicAdd(&a.S->shard_ent[chunk % kShards], tot);
+    if (s_cnt) atomicAdd(&a.S->shard_cnd[chunk % kShards], s_cnt);
+  }
+}
+
+// Candidates of this workgroup's chunk range, kTpc threads per chunk: fn(comp, valid).
+constexpr uint32_t kTpc64 = 16;
+template <typename F>
+__device__ __forceinline__ void for_cands64(const Fast64Args& a, uint32_t c0, uint32_t c1, F&& fn) {
+  const uint32_t cpr = kBlock / kTpc64;
+  for (uint32_t cb = c0; cb < c1; cb += cpr) {
+    const uint32_t c = cb + threadIdx.x / kTpc64, q = threadIdx.x % kTpc64;
+    const uint32_t cnt = c < c1 ? min(a.ccnt[c], (uint32_t)kC64Slot) : 0u;
+    for (uint32_t r = q; r < cnt; r += kTpc64) {
+      const uint64_t* s = reinterpret_cast<const uint64_t*>(&a.cand[(uint64_t)c * kC64Slot + r]);
+      fn(u128_of(s[1], s[0]));
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_resolve64(Fast64Args a) {
+  __shared__ u128 sv[kSmallCap64];                        // 32 KiB: histogram, then sort
+  __shared__ uint32_t s_tmp[8], s_out[4], s_flag, s_cnt, s_base, s_tot[2], s_ovf;
+  uint32_t* h = reinterpret_cast<uint32_t*>(sv);
+  const int tid = threadIdx.x;
+  TopkState* S = a.S;
+  const uint32_t c0 = blockIdx.x * a.per, c1 = min(c0 + a.per, a.nchunks);
+  uint32_t se = 0, sc = 0;
+  if (tid < kShards) { se = S->shard_ent[tid]; sc = S->shard_cnd[tid]; }
+  uint32_t hv[kHistBins / kBlock];
+#pragma unroll
+  for (int j = 0; j < kHistBins / kBlock; ++j) hv[j] = a.chist[j * kBlock + tid];
+  const uint32_t t_lo = S->t_lo, sbin = S->sbin;
+  if (tid < 64) {
+    se = wave_sum(se);
+    sc = wave_sum(sc);
+    if (tid == 0) { s_tot[0] = se; s_tot[1] = sc; s_cnt = 0; s_ovf = 0; }
+  }
+#pragma unroll
+  for (int j = 0; j < kHistBins / kBlock; ++j) h[j * kBlock + tid] = hv[j];
+  __syncthreads();
+  const uint32_t n_ent = s_tot[0], n_cand = s_tot[1], n_hi = n_ent - n_cand;
+  bool retry = n_cand > n_ent || (uint64_t)n_ent < a.k || (uint64_t)n_hi >= a.k;
+  const uint32_t rank = retry ? 0u : (uint32_t)(a.k - n_hi);
+  uint32_t beta = 0, r_in = 1, cnt_beta = 0;
+  if (!retry) {
+    find_rank_desc64(h, rank, s_tmp, s_out);
+    beta = s_out[0]; r_in = s_out[1]; cnt_beta = h[beta];
+    retry = cnt_beta > (uint32_t)kSmallCap64 || cnt_beta < r_in;
+  }
+  __syncthreads();                                        // h (sv) is reused below
+  for (uint32_t c = c0 + tid; c < c1; c += kBlock)
+    if (a.ccnt[c] > (uint32_t)kC64Slot) s_ovf = 1u;
+  __syncthreads();
+  if (s_ovf && tid == 0) st_agent(&S->err, 1u);           // a slot overflowed: exact path
+  if (!retry && !s_ovf) {
+    for_cands64(a, c0, c1, [&](const u128& v) {
+      const uint32_t key = (uint32_t)(v >> 64);           // = key64 >> 32: key32 before the clamp
+      const uint32_t k32 = key > 0x7f800000u ? kNanKey : key;
+      if (((k32 - t_lo) >> sbin) == beta) {
+        const uint32_t q = atomicAdd(&s_cnt, 1u);
+        if (q < (uint32_t)kSmallCap64) sv[q] = v;
+      }
+    });
+    __syncthreads();
+    const uint32_t mine = min(s_cnt, (uint32_t)kSmallCap64);
+    if (tid == 0 && mine) s_base = atomicAdd(&a.E->small_n, mine);
+    __syncthreads();
+    for (uint32_t q = tid; q < mine; q += kBlock) {
+      if (s_base + q < (uint32_t)kSmallCap64) {
+        uint64_t* d = reinterpret_cast<uint64_t*>(&a.small[s_base + q]);
+        st_agent(d, (uint64_t)sv[q]);
+        st_agent(d + 1, (uint64_t)(sv[q] >> 64));
+      }
+    }
+  }
+  if (!last_block_arrive_tree(a.tick, gridDim.x, blockIdx.x, &s_flag)) return;
+  // ---- last workgroup: T = the r_in-th largest of bin beta, status, self-cleaning ----
+  const bool err = ld_agent(&S->err) != 0u;
+  const uint32_t got = ld_agent(&a.E->small_n);
+  retry = retry || err || got != cnt_beta;
+  u128 T = 0;
+  if (!retry) {
+    uint32_t P2 = 1;
+    while (P2 < cnt_beta) P2 <<= 1;
+    for (uint32_t i = tid; i < P2; i += kBlock) {
+      u128 v = 0;
+      if (i < cnt_beta) {
+        const uint64_t* s = reinterpret_cast<const uint64_t*>(&a.small[i]);
+        v = u128_of(ld_agent(s + 1), ld_agent(s));
+      }
+      sv[i] = v;
+    }
+    __syncthreads();
+    bitonic_desc128(sv, P2);
+    T = sv[r_in - 1];
+  }
+  for (int b = tid; b < kHistBins; b += kBlock) st_agent(&a.chist[b], 0u);
+  if (tid == 0) {
+    a.E->p_hi = (uint64_t)(T >> 64); a.E->p_lo = (uint64_t)T;
+    a.E->status = retry ? (uint32_t)FC_STATUS_RETRY_EXACT : (uint32_t)FC_STATUS_OK;
+    a.E->small_n = 0;
+    S->err = 0;
+    *a.status = retry ? (uint32_t)FC_STATUS_RETRY_EXACT : (uint32_t)FC_STATUS_OK;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_fixup64(Fast64Args a) {
+  if (a.E->status != (uint32_t)FC_STATUS_OK) return;
+  const u128 T = u128_of(a.E->p_hi, a.E->p_lo);
+  const uint32_t c0 = blockIdx.x * a.per, c1 = min(c0 + a.per, a.nchunks);
+  for_cands64(a, c0, c1, [&](const u128& v) {
+    if (v < T) a.out[(uint32_t)v] = 0.0;
+  });
+}
+
 template __global__ void k_engine64<kKeyMag>(Engine64Args);
 template __global__ void k_engine64<kKeyPhilox>(Engine64Args);
 template __global__ void k_select_dense64<kKeyMag>(const double*, uint64_t, uint64_t, uint64_t, uint64_t, const Eng64State*, double*);

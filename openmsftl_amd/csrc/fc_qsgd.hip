@@ -10,7 +10,8 @@
 // E[q] = g / tau.)  Exact arithmetic of this build, shared with the oracle:
 //   norm  = sqrt(sum of g_i^2 in fp64), the sum in a fixed order (k_qsgd_norm), stored as a
 //           double in the header's `p` field;
-//   U_i   = (philox_word(i) >> 8) * 2^-24;
+//   U_i   = (w_i >> 8) * 2^-24, w_i = Philox word i of the LINEAR map (counter block i >> 2,
+//           word i & 3: oracle/philox.py linear_words; not the segment map of philox_word);
 //   l_i   = floor(fl64(fl64(s * |g_i|) / norm) + U_i)   in [0, s]; 0 when not finite;
 //   code  = signbit(g_i) << (W - 1) | l_i,  W = 4 (bits <= 2), 8 (<= 6), 16 (<= 14) bits,
 //           packed little-endian, 32 / W codes per uint32;

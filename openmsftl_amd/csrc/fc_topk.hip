@@ -178,10 +178,35 @@ __device__ __forceinline__ void seg_lane(const SamplePlan& P, uint32_t s, int ti
   e = (uint32_t)st + (uint32_t)tid * 4u;
 }
 
+// Sample loads: 4 consecutive elements of g as the float4 whose mag_key gives their keys.
+// float32: the values themselves.  float64 (fc_topk_dense_f64's sampled path, fc_f64.hip): the
+// 31-bit HIGH key of each double (|x| bits >> 32: exponent + 20 mantissa bits) as a float bit
+// pattern, so mag_key of it is that high key (clamped at kNanKey: a non-decreasing map, which is
+// all a bracket needs).
+__device__ __forceinline__ float4 load4_sample(const float* __restrict__ g, uint64_t e, uint64_t n) {
+  return load4_plain(g, e, n);
+}
+__device__ __forceinline__ float hikey_f(double x) {
+  return __uint_as_float((uint32_t)(((uint64_t)__double_as_longlong(x) & 0x7fffffffffffffffull) >> 32));
+}
+__device__ __forceinline__ float4 load4_sample(const double* __restrict__ g, uint64_t e, uint64_t n) {
+  double v[4] = {0.0, 0.0, 0.0, 0.0};
+  if (e + 4 <= n) {
+    const double2 a = *reinterpret_cast<const double2*>(g + e);
+    const double2 b = *reinterpret_cast<const double2*>(g + e + 2);
+    v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (e + j < n) v[j] = g[e + j];
+  }
+  return make_float4(hikey_f(v[0]), hikey_f(v[1]), hikey_f(v[2]), hikey_f(v[3]));
+}
+
 // Pilot level-1 histogram (key >> 19) of the kPilotSegs pilot segments -> the window.
 // own: this workgroup IS workgroup 0 (its segments xs / es / ls are the pilot, already loaded).
-template <int KM, bool OWN_ONLY = false>
-__device__ __forceinline__ FineWin pilot_window(const float* __restrict__ g, const SamplePlan& P,
+template <int KM, bool OWN_ONLY = false, typename T = float>
+__device__ __forceinline__ FineWin pilot_window(const T* __restrict__ g, const SamplePlan& P,
                                                 uint64_t seed, uint64_t off, uint32_t* h,
                                                 uint32_t* s_tmp, uint32_t* s_out, bool own,
                                                 const float4 (&xs)[kSampleSegs],
@@ -201,7 +226,7 @@ __device__ __forceinline__ FineWin pilot_window(const float* __restrict__ g, con
     xp[q] = make_float4(0.f, 0.f, 0.f, 0.f);
     if ((uint32_t)q < P.np) {
       seg_lane(P, pilot_seg(P, (uint32_t)q), tid, ep[q], lp[q]);
-      if (ep[q] < lp[q]) xp[q] = load4_plain(g, ep[q], lp[q]);
+      if (ep[q] < lp[q]) xp[q] = load4_sample(g, ep[q], lp[q]);
     }
   }
   __syncthreads();                                  // h zeroed by the caller
@@ -242,8 +267,8 @@ struct SampleShared {
 // written, publish it to the compaction workgroups of the same launch (S->fz_pub = pub).
 // SHARED_ONLY: the launch is a lone client's (the window always comes from workgroup 0's own
 // segments): no second set of pilot registers (k_fused_mag runs in 64 VGPRs)
-template <int KM, bool SHARED_ONLY = false>
-__device__ __forceinline__ void sample_body(const float* __restrict__ g, const SamplePlan& P,
+template <int KM, bool SHARED_ONLY = false, typename T = float>
+__device__ __forceinline__ void sample_body(const T* __restrict__ g, const SamplePlan& P,
                                             uint64_t seed, uint64_t off, const WsPtrs& W,
                                             uint32_t ib, fc_packet_hdr* hdr, const HdrInit& HI,
                                             uint32_t bid, uint32_t nb, bool shared_pilot,
@@ -255,24 +280,33 @@ __device__ __forceinline__ void sample_body(const float* __restrict__ g, const S
   TopkState* S = W.st;
   const int tid = threadIdx.x;
   FC_TR(0);
-  // this workgroup's segments first (plain loads: ~2 us sooner than non-temporal here)
+  // The sample is P.pstride groups of kSampleSegs segments (group v: segments v + q * pstride;
+  // group 0 is the pilot).  Workgroup bid of nb takes groups bid, bid + nb, ... one after the
+  // other into the same histogram: a batched launch gives each workgroup FC_SAMPLE_ROUNDS = 4
+  // (a quarter of the workgroups, one window, one flush and one ticket per four groups; the
+  // launch was occupancy-bound at ~17 us per workgroup: 64 x 128 M 190 -> 125 us, 64 x 16 M
+  // 84 -> 59 us).  The sample, its window and so the bracket are unchanged.
   float4 xs[kSampleSegs];
   uint32_t es[kSampleSegs], ls[kSampleSegs];
+  auto load_group = [&](uint32_t v) {
 #pragma unroll
-  for (int q = 0; q < kSampleSegs; ++q) {
-    const uint32_t s = bid + (uint32_t)q * nb;
-    es[q] = ls[q] = 0;
-    xs[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (s < P.nseg) {
-      seg_lane(P, s, tid, es[q], ls[q]);
-      if (es[q] < ls[q]) xs[q] = load4_plain(g, es[q], ls[q]);
+    for (int q = 0; q < kSampleSegs; ++q) {
+      const uint32_t s = v + (uint32_t)q * P.pstride;
+      es[q] = ls[q] = 0;
+      xs[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (s < P.nseg) {
+        seg_lane(P, s, tid, es[q], ls[q]);
+        if (es[q] < ls[q]) xs[q] = load4_sample(g, es[q], ls[q]);
+      }
     }
-  }
+  };
+  // this workgroup's first group first (plain loads: ~2 us sooner than non-temporal here)
+  load_group(bid);
   for (int b = tid; b < kHistBins; b += kBlock) h[b] = 0;
   FineWin F;
   if (SHARED_ONLY) shared_pilot = true;
   if (!shared_pilot || bid == 0) {
-    F = pilot_window<KM, SHARED_ONLY>(g, P, seed, off, h, s_tmp, s_out, bid == 0, xs, es, ls);
+    F = pilot_window<KM, SHARED_ONLY, T>(g, P, seed, off, h, s_tmp, s_out, bid == 0, xs, es, ls);
     if (shared_pilot && tid == 0) {               // publish: sc1 payload, drained, sc1 flag
       st_agent(&S->win_klo, F.klo); st_agent(&S->win_khi, F.khi); st_agent(&S->win_fs, F.fs);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -296,14 +330,19 @@ __device__ __forceinline__ void sample_body(const float* __restrict__ g, const S
   __syncthreads();
   FC_TR(2);
   // ---- this workgroup's share of the sample ----
+  for (uint32_t v = bid;;) {
 #pragma unroll
-  for (int q = 0; q < kSampleSegs; ++q) {
-    if (es[q] < ls[q]) {
-      const uint4 kk = keys4<KM>(xs[q], es[q], seed, off);
+    for (int q = 0; q < kSampleSegs; ++q) {
+      if (es[q] < ls[q]) {
+        const uint4 kk = keys4<KM>(xs[q], es[q], seed, off);
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (es[q] + j < ls[q]) atomicAdd(&h[fine_bin(u4get(kk, j), F)], 1u);
+        for (int j = 0; j < 4; ++j)
+          if (es[q] + j < ls[q]) atomicAdd(&h[fine_bin(u4get(kk, j), F)], 1u);
+      }
     }
+    v += nb;
+    if (SHARED_ONLY || v >= P.pstride) break;    // (k_fused_mag: one group per workgroup)
+    load_group(v);
   }
   __syncthreads();
   FC_TR(3);
@@ -367,7 +406,7 @@ __device__ __forceinline__ void sample_body(const float* __restrict__ g, const S
 }
 
 template <int KM>
-__global__ __launch_bounds__(kBlock) void k_sample1(const float* __restrict__ g, SamplePlan P,
+__global__ __launch_bounds__(kBlock, 8) void k_sample1(const float* __restrict__ g, SamplePlan P,
                                                     uint64_t seed, uint64_t off, WsPtrs W,
                                                     uint32_t ib, fc_packet_hdr* hdr, HdrInit HI,
                                                     const fc_encode_job* jobs,
@@ -990,9 +1029,16 @@ template __global__ void k_fused_mag<true>(CompactArgs, SamplePlan, HdrInit, uin
 // LISTED element (comp >= L64); the slack ones (comp < T64) must go back to +0.  Every slack
 // entry is a candidate of its chunk, so the workgroups that gathered a chunk range wait for the
 // last one to publish T64 (generation counter, release/acquire) and zero the slack of their
-// own range: no fix-up launch (it took 13.8 us per 128 M gradient as its own kernel).  The
-// wait is safe: the grid (<= 512 workgroups, 4 per CU by LDS) is always co-resident, and the
-// spin is bounded (FC_STATUS_TIMEOUT, never expected).
+// own range: no fix-up launch (it took 13.8 us per 128 M gradient as its own kernel).
+// The in-kernel waits (beta, "gathered", T64) need every workgroup of a client resident while
+// any of them spins.  A lone encode's grid is <= 512 workgroups (4 per CU by LDS: 1024 slots).
+// A batched launch dispatches its grid in order (x = the client's workgroups, fastest), so at
+// most its LAST client is partly dispatched, and the complete clients before it free the slots
+// it waits for.  Two batched launches on concurrent streams could each hold a partly
+// dispatched client: harmless at <= kResolveGridBatch (16) workgroups per client, so the host
+// side (codec.encode_top_batch) runs batches above 2^27 elements per client, whose clients get
+// up to 512 workgroups (resolve_grid), on ONE stream.  Every spin is bounded (FC_STATUS_TIMEOUT
+// -> the exact path; never expected).
 // --------------------------------------------------------------------------------------
 struct ResolveArgs {
   uint32_t ib, nchunks;

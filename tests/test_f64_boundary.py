@@ -274,3 +274,58 @@ def test_gpu_fedavg_weight_dtypes():
     pk = [codec.encode_top(torch.from_numpy(r).cuda(), 100) for r in Gm]
     with pytest.raises(TypeError):
         f.aggregate_packets(pk)
+
+
+# ---- the sampled fp64 path (fc_topk_dense_f64_sampled) against the exact radix select ------
+def _f64_inputs(kind, n, seed):
+    rng = np.random.default_rng(seed)
+    if kind == "gauss":
+        return rng.standard_normal(n) * 10.0 ** rng.uniform(-4, -1)
+    if kind == "layers":                       # per-"layer" scales 1e-6 .. 1e2
+        g = rng.standard_normal(n)
+        cuts = np.sort(rng.choice(n, 7, replace=False))
+        for j, (a, b) in enumerate(zip(np.r_[0, cuts], np.r_[cuts, n])):
+            g[a:b] *= 10.0 ** (j - 6)
+        return g
+    if kind == "lowbits":                      # many values share their high 32 key bits
+        return 1.0 + rng.integers(0, 1 << 20, n) * 2.0 ** -52 * rng.choice([-1.0, 1.0], n)
+    if kind == "special":
+        g = rng.standard_normal(n)
+        g[rng.integers(0, n, 50)] = np.inf
+        g[rng.integers(0, n, 50)] = -np.inf
+        g[rng.integers(0, n, 50)] = np.nan
+        g[rng.random(n) < 0.05] = -0.0
+        return g
+    raise ValueError(kind)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["gauss", "layers", "lowbits", "special"])
+@pytest.mark.parametrize("n,f", [((1 << 20) + 3, 0.1), (3_000_001, 0.01), (16_777_216 + 5, 0.1)])
+def test_gpu_sampled_top_f64_equals_exact(kind, n, f):
+    """Sampled bracket + one streaming pass + exact candidate select gives the exact radix
+    select's bytes; on Gaussian-like gradients without a retry."""
+    import torch
+    from openmsftl_amd import codec
+    g = torch.from_numpy(_f64_inputs(kind, n, n % 1000)).cuda()
+    k = co.num_kept(f, n)
+    want = codec.compress_top_dense_f64(g, k, exact=True)
+    got = codec.compress_top_dense_f64(g, k, check=False)
+    redo = codec.resolve_f64(got)
+    assert got.cpu().numpy().tobytes() == want.cpu().numpy().tobytes()
+    if kind in ("gauss", "layers"):
+        assert redo == 0, "sampled bracket missed on a Gaussian-like gradient"
+
+
+@pytest.mark.gpu
+def test_gpu_sampled_top_f64_vs_oracle_and_reuse():
+    """3 M Gaussian, f = 0.1: the oracle's bytes, twice on one workspace (self-cleaning)."""
+    import torch
+    from openmsftl_amd import codec
+    n, f = 3_000_017, 0.1
+    g = _f64_inputs("gauss", n, 9)
+    want = co.compress({"compression_function": "top", "fraction_coordinate": f}, g.copy())
+    gd = torch.from_numpy(g).cuda()
+    for _ in range(2):
+        got = codec.compress_top_dense_f64(gd, co.num_kept(f, n))
+        assert got.cpu().numpy().tobytes() == want.tobytes()

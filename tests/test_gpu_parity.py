@@ -29,7 +29,7 @@ def _gpu():
         pytest.skip("no GPU")
     from openmsftl_amd import _lib
     lib = _lib.load()
-    assert lib.fc_abi_version() == 3
+    assert lib.fc_abi_version() == 4
 
 
 def _codec():

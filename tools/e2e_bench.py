@@ -1,17 +1,41 @@
-"""End-to-end (PCIe-inclusive) FedAVG rate: host gradients -> H2D -> encode -> decode-accumulate
--> D2H, BASELINE.json configs[4] per-GPU shard (512 clients x 25,557,032 fp32, top f = 0.01 —
-the highest compression ratio the reference's codecs offer, 50x packets).
+"""End-to-end (PCIe-inclusive) FedAVG rate, BASELINE.json configs[4]: host gradients -> H2D ->
+top-k encode -> decode-accumulate -> cross-GPU combine -> D2H, at 1..N GPUs.
 
-    python tools/e2e_bench.py [--clients 512] [--n 25557032] [--f 0.01] [--group 64]
+    python tools/e2e_bench.py [--gpus N] [--mode ring|reduce|chain] [--clients 512] \
+        [--n 25557032] [--f 0.01] [--group 64]
 
-The reference path starts and ends in host memory (client.py:53 flattens to NumPy; the
-aggregate goes back to the server model, aggregation.py:99), so this is the rate a drop-in
-user sees.  Pipeline: a copy stream streams each client's pinned host gradient into a ring of
-device slots (H2D overlapped with the previous clients' encodes); the compute stream encodes
-into a ring of `--group` packets and folds each full group into the running aggregate
-(fc_decode_accumulate_continue keeps the fold bit-identical to one call over all rows); the
-aggregate is copied D2H at the end.  `--host-pool` distinct pinned gradients are cycled
-(each client's H2D is still a real PCIe transfer).  Prints one JSON line.
+configs[4] is "8 x MI355X: 4096 clients x 25.5 M-param gradients, highest compression ratio
+(top f = 0.01: 50x packets), end-to-end H2D -> encode -> reduce -> decode -> D2H timed": per
+GPU 512 clients (``--clients`` is per GPU; M = clients x N in all).  The reference's round
+starts and ends in host memory (client.py:53 flattens to NumPy; the aggregate goes back to the
+server model, aggregation.py:99), so this is the rate a drop-in user sees.
+
+One process per GPU: with ``--gpus N`` and no WORLD_SIZE in the environment the ranks are
+started as child processes before anything touches the GPU (bench.spawn_ranks); under
+torch.distributed.run it runs as one rank.  Every rank streams its clients' host gradients
+through openmsftl_amd.pipeline.HostFedAvg (ring of device slots on a copy stream, encodes on
+the compute stream, packet folds per group of ``--group``); the combine is
+
+* ``ring`` (default): openmsftl_amd.pipeline.RankRing — the fold groups of the M rows are dealt
+  round-robin to the ranks and the running aggregate travels rank to rank in group order
+  (send/recv: RCCL over xGMI), so the result is the single-GPU fold bit for bit (gar.py:44)
+  while every rank's H2D + encodes run in parallel;
+* ``reduce``: contiguous shards (server.py:74 order) folded locally, then ONE fp32 sum-reduce
+  (RCCL) of the partial aggregates to rank 0 (distributed.py's reassociation bound);
+* ``chain``: contiguous shards, each rank continuing the previous rank's fold (bit-exact,
+  serial across ranks).
+
+Then rank 0 copies the aggregate D2H.  Timed: barrier + device sync on both sides of each
+round, the MAX over ranks; ``value`` = client gradient bytes (4 N per client, all ranks) per
+second.  ``h2d_alone_GBps`` is a lone pinned H2D of the same gradients on each rank (its PCIe
+ceiling), ``pcie_frac`` = value / the sum of those.
+
+Host memory: 512 x 102 MB per GPU will not fit in RAM, so each rank cycles a pool of
+``--host-pool`` distinct pinned gradients (client i = pool[i % P]; every client's H2D is
+still a real PCIe transfer of its 102 MB).  ``--source configs4`` instead feeds the committed
+configs[4] parity inputs (tests/golden/make_digests_full.py: 70 clients, each rank generating
+only the rows it streams) and ``--dump-agg`` saves rank 0's aggregate: tests/test_e2e_multirank.py
+checks it against the oracle's digest.  Prints one JSON line (rank 0).
 """
 from __future__ import annotations
 
@@ -25,65 +49,162 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def main():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--clients", type=int, default=512)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
+                    help="nccl (RCCL over xGMI) or gloo (rehearsal: ranks may share a GPU)")
+    ap.add_argument("--mode", default="ring", choices=("ring", "reduce", "chain"))
+    ap.add_argument("--clients", type=int, default=512, help="clients per GPU (synthetic)")
     ap.add_argument("--n", type=int, default=25_557_032)
     ap.add_argument("--f", type=float, default=0.01)
     ap.add_argument("--group", type=int, default=64)
     ap.add_argument("--ring", type=int, default=4, help="device gradient slots")
     ap.add_argument("--host-pool", type=int, default=8)
     ap.add_argument("--reps", type=int, default=2)
-    args = ap.parse_args()
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--source", default="synthetic", choices=("synthetic", "configs4"))
+    ap.add_argument("--dump-agg", default=None, help="rank 0 saves the aggregate (.npy)")
+    return ap.parse_args(argv)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def rows_needed(mode, M, W, r, group):
+    """The global rows rank r streams (server.py:74 order)."""
+    from openmsftl_amd.distributed import shard_range
+    from openmsftl_amd.pipeline import group_bounds
+    if mode == "ring":
+        return [i for t, g in enumerate(group_bounds(M, group)) if t % W == r for i in g]
+    return list(shard_range(M, W, r))
+
+
+def main():
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        import bench
+        sys.exit(bench.spawn_ranks(sys.argv[1:], args.gpus, script=os.path.abspath(__file__)))
     import numpy as np
     import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
+    if args.backend == "gloo":
+        local %= max(1, torch.cuda.device_count())
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    if world > 1:
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     from openmsftl_amd.compression import kept_count
-    from openmsftl_amd.distributed import fedavg_weights
+    from openmsftl_amd.distributed import ShardedFedAvg, fedavg_weights
+    from openmsftl_amd.pipeline import HostFedAvg, RankRing, host_fold
 
-    from openmsftl_amd.pipeline import HostFedAvg
-
-    dev = torch.device("cuda", 0)
-    n, C, Gs, R = args.n, args.clients, args.group, args.ring
-    k = kept_count(args.f, n)
     t0 = time.perf_counter()
-    host = []
-    for i in range(args.host_pool):
-        g = torch.randn(n, generator=torch.Generator().manual_seed(1000 + i))
-        g.mul_(10.0 ** np.random.default_rng(i).uniform(-4, -1))
-        host.append(g.pin_memory())
-    print(f"[e2e] host pool ready in {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
-    pipe = HostFedAvg(n, k, group=Gs, ring=R, device=dev)
-    w = fedavg_weights(C)
+    if args.source == "configs4":
+        sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+        import make_digests_full as MD
+        w4 = MD.WORKLOADS["configs4"]
+        M, n, frac = w4["clients"], w4["n"], w4["fraction"]
+        mine = rows_needed(args.mode, M, world, rank, args.group)
+        data = {i: torch.from_numpy(MD.fullsize_grad("configs4", i)).pin_memory() for i in mine}
+        get = data.__getitem__
+        pool = [data[i] for i in mine[:args.host_pool]]
+    else:
+        M, n, frac = args.clients * world, args.n, args.f
+        pool = []
+        for i in range(args.host_pool):
+            g = torch.randn(n, generator=torch.Generator().manual_seed(1000 + 97 * rank + i))
+            g.mul_(float(10.0 ** np.random.default_rng(97 * rank + i).uniform(-4, -1)))
+            pool.append(g.pin_memory())
+        get = lambda i: pool[i % len(pool)]          # noqa: E731
+    log(f"[e2e rank {rank}] host inputs ready in {time.perf_counter() - t0:.1f} s")
+    k = kept_count(frac, n)
+    w = fedavg_weights(M)
+    pipe = HostFedAvg(n, k, group=args.group, ring=args.ring, device=dev,
+                      sets=2 if args.mode == "ring" else 1)
+    out_host = torch.empty(n, dtype=torch.float32).pin_memory()
+    if args.mode == "ring":
+        rr = RankRing(pipe, dst=0)
+        combine = lambda: rr.run(get, M, w)          # noqa: E731
+    else:
+        sh = ShardedFedAvg(mode=args.mode, dst=0)
+        fold = host_fold(pipe, get)
+        acc = torch.empty(n, dtype=torch.float32, device=dev)
+        combine = lambda: sh.aggregate(fold, M, acc, weights=w)   # noqa: E731
 
-    def run():
-        before = pipe.exact_fallbacks
-        pipe.run(lambda i: host[i % len(host)], C, w)
-        return pipe.exact_fallbacks - before
+    def one_round():
+        res = combine()
+        if rank == 0:                                # D2H of the aggregate, rank 0
+            out_host.copy_(res, non_blocking=True)
+        torch.cuda.synchronize(dev)
 
-    run()                                             # warm-up (allocations, code objects)
-    times, redo = [], 0
+    def barrier():
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        one_round()
+    times = []
     for _ in range(args.reps):
-        torch.cuda.synchronize()
+        barrier()
         t = time.perf_counter()
-        redo += run()
+        one_round()
+        barrier()
         times.append(time.perf_counter() - t)
     dt = min(times)
-    h2d_bytes = 4.0 * n * C
-    line = {"metric": "end-to-end FedAVG (H2D -> top-k encode -> decode-accumulate -> D2H) GB/s",
-            "value": round(h2d_bytes / dt / 1e9, 2), "unit": "GB/s (client gradient bytes)",
-            "seconds": round(dt, 4), "all_reps_s": [round(x, 4) for x in times],
-            "clients": C, "n": n, "k": k, "fraction": args.f, "group": Gs, "ring": R,
-            "h2d_GB": round(h2d_bytes / 1e9, 2), "exact_fallbacks": redo,
-            "host_pool": len(host)}
-    # PCIe ceiling for reference: one pinned H2D of one gradient, alone
-    torch.cuda.synchronize()
+    if world > 1:                                    # max over ranks of each rank's best
+        tt = torch.tensor([dt, float(pipe.exact_fallbacks)], dtype=torch.float64)
+        if args.backend == "nccl":
+            tt = tt.to(dev)
+        dist.all_reduce(tt[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(tt[1:], op=dist.ReduceOp.SUM)
+        dt, redo = float(tt[0].item()), int(tt[1].item())
+    else:
+        redo = pipe.exact_fallbacks
+    # this rank's PCIe ceiling: pinned H2D of its pool alone
+    torch.cuda.synchronize(dev)
     t = time.perf_counter()
-    for i in range(8):
-        pipe.slots[0].copy_(host[i % len(host)], non_blocking=True)
-    torch.cuda.synchronize()
-    line["h2d_alone_GBps"] = round(8 * 4.0 * n / (time.perf_counter() - t) / 1e9, 2)
-    print(json.dumps(line), flush=True)
+    reps = 8
+    for i in range(reps):
+        pipe.slots[i % pipe.ring].copy_(pool[i % len(pool)], non_blocking=True)
+    torch.cuda.synchronize(dev)
+    h2d = reps * 4.0 * n / (time.perf_counter() - t) / 1e9
+    h2d_all = [h2d]
+    if world > 1:
+        obj = [None] * world
+        dist.all_gather_object(obj, h2d)
+        h2d_all = obj
+    if args.dump_agg and rank == 0:
+        np.save(args.dump_agg, out_host.numpy())
+    if rank == 0:
+        value = 4.0 * n * M / dt / 1e9
+        line = {"metric": "end-to-end FedAVG (H2D -> top-k encode -> decode-accumulate -> "
+                          "cross-GPU combine -> D2H) GB/s",
+                "value": round(value, 2), "unit": "GB/s (client gradient bytes, all GPUs)",
+                "n_gpus": world, "mode": args.mode, "backend": args.backend,
+                "seconds": round(dt, 4), "all_reps_s_rank0": [round(x, 4) for x in times],
+                "clients": M, "clients_per_gpu": M / world, "n": n, "k": k, "fraction": frac,
+                "group": args.group, "ring": args.ring, "h2d_GB": round(4.0 * n * M / 1e9, 2),
+                "exact_fallbacks": redo, "source": args.source,
+                "host_pool_per_rank": len(pool),
+                "h2d_alone_GBps": [round(x, 2) for x in h2d_all],
+                "pcie_frac": round(value / sum(h2d_all), 4),
+                "config": "BASELINE configs[4]: %d clients x %d fp32, top f=%g, end-to-end"
+                          % (M, n, frac)}
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":
