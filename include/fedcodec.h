@@ -289,8 +289,8 @@ int fc_qsgd_decode_accumulate(const fc_packet_view* views_dev, int m, uint64_t n
  *   writes out and lists the bracket's candidates, exact select among them, slack fix-up
  *   (replaces compression.py:31-37 for float64 client.grad; 8N read + 8N written instead of
  *   <= 8 passes of 8N).  Writes *status (DEVICE uint32) = FC_STATUS_OK, or
- *   FC_STATUS_RETRY_EXACT when the bracket missed / a chunk's candidate slot overflowed: out
- *   is then not valid and the caller runs fc_topk_dense_f64 (exact).  Same result bits as
+ *   FC_STATUS_RETRY_EXACT when the bracket missed (or > 2048 candidates share the rank's
+ *   histogram bin): out is then not valid and the caller runs fc_topk_dense_f64 (exact).  Same result bits as
  *   fc_topk_dense_f64.  ws: fc_workspace_bytes(n), zeroed once. */
 int fc_topk_dense_f64_sampled(const double* g, uint64_t n, uint64_t k, double* out, void* ws,
                               size_t ws_bytes, uint32_t* status, fc_stream_t stream);

@@ -815,7 +815,9 @@ int fc_topk_dense_f64_sampled(const double* g, uint64_t n, uint64_t k, double* o
   Fast64Args a;
   memset(&a, 0, sizeof a);
   a.g = g; a.n = n; a.k = k; a.nchunks = (uint32_t)Lw.nchunks;
-  a.per = 16;                                    // chunks per resolve / fix-up workgroup
+  // chunks per k_resolve64 workgroup: >= 16, and <= kResolve64Grid workgroups (they wait for
+  // each other's T in-kernel)
+  a.per = (uint32_t)std::max<uint64_t>(16, (Lw.nchunks + kResolve64Grid - 1) / kResolve64Grid);
   a.S = W.st; a.E = reinterpret_cast<Eng64State*>(static_cast<char*>(ws) + kEng64Off);
   a.ccnt = W.ccnt; a.cand = reinterpret_cast<u128*>(W.cand); a.chist = W.chist;
   a.tick = W.tick + 2 * kTickWords; a.small = reinterpret_cast<u128*>(W.small);
@@ -836,8 +838,6 @@ int fc_topk_dense_f64_sampled(const double* g, uint64_t n, uint64_t k, double* o
     TimedLaunch t(FC_TIME_ENGINE, s);
     hipLaunchKernelGGL(k_resolve64, dim3(rgrid), dim3(kBlock), 0, s, a);
     FC_LAUNCHED("k_resolve64");
-    hipLaunchKernelGGL(k_fixup64, dim3(rgrid), dim3(kBlock), 0, s, a);
-    FC_LAUNCHED("k_fixup64");
   }
   return FC_OK;
 }

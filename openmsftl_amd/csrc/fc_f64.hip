@@ -38,7 +38,8 @@ __device__ __forceinline__ u128 comp64(const double* g, uint64_t i, uint64_t see
 // Engine state, in the encoder workspace's state block after TopkState.
 struct Eng64State {
   uint64_t p_hi, p_lo;                       // resolved high bits of T (u128 as two halves)
-  uint32_t shift, rank, matched, done, status, ticket, small_n, pad_;
+  uint32_t shift, rank, matched, done, status, ticket, small_n;
+  uint32_t gen;                              // k_resolve64: bumped once T is published
 };
 static_assert(sizeof(TopkState) + sizeof(Eng64State) <= 1024, "state block");
 constexpr uint64_t kEng64Off = 768;
@@ -300,12 +301,17 @@ __global__ __launch_bounds__(kBlock) void k_div_scalar64(double* x, uint64_t n, 
 //                 candidate's exact comp into its chunk's slot, its bin into the histogram
 //   k_resolve64   rank r = k - #definite among the candidates: every workgroup finds the bin
 //                 beta holding it (the histogram, from L2) and gathers its chunks' candidates
-//                 in beta; the last arriver sorts them (<= 2048, LDS) and picks T, the exact
-//                 k-th largest comp; any miss (bracket, slot overflow, big bin) -> RETRY
-//   k_fixup64     q[idx] = +0 for every candidate with comp < T
+//                 in beta (a chunk whose candidates overflowed its slot is rescanned from
+//                 g); the last arriver sorts them (<= 2048, LDS) and picks T, the exact k-th
+//                 largest comp; a bracket that missed or a bin beta above 2048 -> RETRY
+//                 and publishes it (generation word); every workgroup then sets q[idx] = +0
+//                 for its candidates with comp < T (the grid, <= 256 workgroups, is
+//                 co-resident; the wait is bounded)
 // The exact radix engine (<= 8 passes of 8N) stays the fallback and serves native rand-k.
 // --------------------------------------------------------------------------------------
 constexpr int kC64Slot = 128;                  // candidate comps per chunk (the 2 KB slot)
+constexpr uint32_t kSpinMax64 = 1u << 18;      // bounded waits (~60 ms): one that ends is a bug
+constexpr uint32_t kResolve64Grid = 256;       // k_resolve64 workgroups at most (co-resident)
 constexpr uint64_t kHdr64Off = 896;            // the sample's scratch packet header
 static_assert(kEng64Off + sizeof(Eng64State) <= kHdr64Off && kHdr64Off + sizeof(fc_packet_hdr) <= 1024,
               "state block layout");
@@ -324,7 +330,7 @@ __global__ __launch_bounds__(kBlock, 8) void k_sample64(const double* __restrict
 struct Fast64Args {
   const double* g;
   uint64_t n, k;
-  uint32_t nchunks, per;       // per: chunks per k_resolve64 / k_fixup64 workgroup
+  uint32_t nchunks, per;       // per: chunks per k_resolve64 workgroup
   TopkState* S;
   Eng64State* E;
   uint32_t* ccnt;              // candidates per chunk (may exceed kC64Slot: overflowed)
@@ -401,44 +407,61 @@ __global__ __launch_bounds__(kBlock) void k_compact64(Fast64Args a) {
     uint32_t tot = 0;
 #pragma unroll
     for (int w = 0; w < kBlock / 64; ++w) tot += s_red[w];
+    if (chunk == 0) *a.status = (uint32_t)FC_STATUS_OK;   // this call's status (k_resolve64)
     a.ccnt[chunk] = s_cnt;
     atomicAdd(&a.S->shard_ent[chunk % kShards], tot);
     if (s_cnt) atomicAdd(&a.S->shard_cnd[chunk % kShards], s_cnt);
   }
 }
 
-// Candidates of this workgroup's chunk range, kTpc threads per chunk: fn(comp, valid).
+// fn(comp) for every candidate of this workgroup's chunk range: kTpc64 threads per chunk read
+// its candidate slot; a chunk whose candidates overflowed the slot (a dense bracket region, a
+// small n's wide bracket) is rescanned from g by the whole workgroup instead.
 constexpr uint32_t kTpc64 = 16;
 template <typename F>
-__device__ __forceinline__ void for_cands64(const Fast64Args& a, uint32_t c0, uint32_t c1, F&& fn) {
+__device__ __forceinline__ void for_cands64(const Fast64Args& a, uint32_t c0, uint32_t c1,
+                                            uint32_t t_lo, uint32_t t_hi, F&& fn) {
   const uint32_t cpr = kBlock / kTpc64;
   for (uint32_t cb = c0; cb < c1; cb += cpr) {
     const uint32_t c = cb + threadIdx.x / kTpc64, q = threadIdx.x % kTpc64;
-    const uint32_t cnt = c < c1 ? min(a.ccnt[c], (uint32_t)kC64Slot) : 0u;
+    uint32_t cnt = c < c1 ? a.ccnt[c] : 0u;
+    if (cnt > (uint32_t)kC64Slot) cnt = 0;                 // rescanned below
     for (uint32_t r = q; r < cnt; r += kTpc64) {
       const uint64_t* s = reinterpret_cast<const uint64_t*>(&a.cand[(uint64_t)c * kC64Slot + r]);
       fn(u128_of(s[1], s[0]));
+    }
+  }
+  for (uint32_t c = c0; c < c1; ++c) {
+    if (a.ccnt[c] <= (uint32_t)kC64Slot) continue;         // (uniform)
+    const uint64_t base = (uint64_t)c * kChunk;
+    for (uint32_t r = threadIdx.x; r < (uint32_t)kChunk; r += kBlock) {
+      const uint64_t e = base + r;
+      if (e >= a.n) break;
+      const double v = a.g[e];
+      const uint32_t key = key32_of(v);
+      if (key >= t_lo && key <= t_hi) fn(((u128)mag_key64(v) << 32) | (u128)(uint32_t)e);
     }
   }
 }
 
 __global__ __launch_bounds__(kBlock) void k_resolve64(Fast64Args a) {
   __shared__ u128 sv[kSmallCap64];                        // 32 KiB: histogram, then sort
-  __shared__ uint32_t s_tmp[8], s_out[4], s_flag, s_cnt, s_base, s_tot[2], s_ovf;
+  __shared__ uint32_t s_tmp[8], s_out[4], s_flag, s_cnt, s_base, s_tot[2];
   uint32_t* h = reinterpret_cast<uint32_t*>(sv);
   const int tid = threadIdx.x;
   TopkState* S = a.S;
   const uint32_t c0 = blockIdx.x * a.per, c1 = min(c0 + a.per, a.nchunks);
+  const uint32_t gen0 = ld_agent(&a.E->gen);              // before the ticket: stable
   uint32_t se = 0, sc = 0;
   if (tid < kShards) { se = S->shard_ent[tid]; sc = S->shard_cnd[tid]; }
   uint32_t hv[kHistBins / kBlock];
 #pragma unroll
   for (int j = 0; j < kHistBins / kBlock; ++j) hv[j] = a.chist[j * kBlock + tid];
-  const uint32_t t_lo = S->t_lo, sbin = S->sbin;
+  const uint32_t t_lo = S->t_lo, t_hi = S->t_hi, sbin = S->sbin;
   if (tid < 64) {
     se = wave_sum(se);
     sc = wave_sum(sc);
-    if (tid == 0) { s_tot[0] = se; s_tot[1] = sc; s_cnt = 0; s_ovf = 0; }
+    if (tid == 0) { s_tot[0] = se; s_tot[1] = sc; s_cnt = 0; }
   }
 #pragma unroll
   for (int j = 0; j < kHistBins / kBlock; ++j) h[j * kBlock + tid] = hv[j];
@@ -453,12 +476,8 @@ __global__ __launch_bounds__(kBlock) void k_resolve64(Fast64Args a) {
     retry = cnt_beta > (uint32_t)kSmallCap64 || cnt_beta < r_in;
   }
   __syncthreads();                                        // h (sv) is reused below
-  for (uint32_t c = c0 + tid; c < c1; c += kBlock)
-    if (a.ccnt[c] > (uint32_t)kC64Slot) s_ovf = 1u;
-  __syncthreads();
-  if (s_ovf && tid == 0) st_agent(&S->err, 1u);           // a slot overflowed: exact path
-  if (!retry && !s_ovf) {
-    for_cands64(a, c0, c1, [&](const u128& v) {
+  if (!retry) {
+    for_cands64(a, c0, c1, t_lo, t_hi, [&](const u128& v) {
       const uint32_t key = (uint32_t)(v >> 64);           // = key64 >> 32: key32 before the clamp
       const uint32_t k32 = key > 0x7f800000u ? kNanKey : key;
       if (((k32 - t_lo) >> sbin) == beta) {
@@ -478,7 +497,24 @@ __global__ __launch_bounds__(kBlock) void k_resolve64(Fast64Args a) {
       }
     }
   }
-  if (!last_block_arrive_tree(a.tick, gridDim.x, blockIdx.x, &s_flag)) return;
+  auto fixup = [&](const u128& T) {
+    for_cands64(a, c0, c1, t_lo, t_hi, [&](const u128& v) {
+      if (v < T) a.out[(uint32_t)v] = 0.0;
+    });
+  };
+  if (!last_block_arrive_tree(a.tick, gridDim.x, blockIdx.x, &s_flag)) {
+    if (retry) return;                                    // (grid-uniform bracket miss)
+    if (tid == 0) {                                       // relaxed sc1 poll (bounded)
+      uint32_t it = 0;
+      while (ld_agent(&a.E->gen) == gen0 && ++it < kSpinMax64) __builtin_amdgcn_s_sleep(4);
+      s_flag = it < kSpinMax64 && ld_agent(&a.E->status) == (uint32_t)FC_STATUS_OK;
+      if (it >= kSpinMax64) atomicMax(a.status, (uint32_t)FC_STATUS_RETRY_EXACT);
+    }
+    __syncthreads();
+    if (!s_flag) return;
+    fixup(u128_of(ld_agent(&a.E->p_hi), ld_agent(&a.E->p_lo)));
+    return;
+  }
   // ---- last workgroup: T = the r_in-th largest of bin beta, status, self-cleaning ----
   const bool err = ld_agent(&S->err) != 0u;
   const uint32_t got = ld_agent(&a.E->small_n);
@@ -501,21 +537,16 @@ __global__ __launch_bounds__(kBlock) void k_resolve64(Fast64Args a) {
   }
   for (int b = tid; b < kHistBins; b += kBlock) st_agent(&a.chist[b], 0u);
   if (tid == 0) {
-    a.E->p_hi = (uint64_t)(T >> 64); a.E->p_lo = (uint64_t)T;
-    a.E->status = retry ? (uint32_t)FC_STATUS_RETRY_EXACT : (uint32_t)FC_STATUS_OK;
+    const uint32_t st = retry ? (uint32_t)FC_STATUS_RETRY_EXACT : (uint32_t)FC_STATUS_OK;
+    st_agent(&a.E->p_hi, (uint64_t)(T >> 64)); st_agent(&a.E->p_lo, (uint64_t)T);
+    st_agent(&a.E->status, st);
     a.E->small_n = 0;
     S->err = 0;
-    *a.status = retry ? (uint32_t)FC_STATUS_RETRY_EXACT : (uint32_t)FC_STATUS_OK;
+    atomicMax(a.status, st);                              // (k_compact64 reset it to OK)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    st_agent(&a.E->gen, gen0 + 1u);                       // T and status first
   }
-}
-
-__global__ __launch_bounds__(kBlock) void k_fixup64(Fast64Args a) {
-  if (a.E->status != (uint32_t)FC_STATUS_OK) return;
-  const u128 T = u128_of(a.E->p_hi, a.E->p_lo);
-  const uint32_t c0 = blockIdx.x * a.per, c1 = min(c0 + a.per, a.nchunks);
-  for_cands64(a, c0, c1, [&](const u128& v) {
-    if (v < T) a.out[(uint32_t)v] = 0.0;
-  });
+  if (!retry) fixup(T);
 }
 
 template __global__ void k_engine64<kKeyMag>(Engine64Args);

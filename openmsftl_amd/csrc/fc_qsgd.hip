@@ -12,7 +12,9 @@
 //           double in the header's `p` field;
 //   U_i   = (w_i >> 8) * 2^-24, w_i = Philox word i of the LINEAR map (counter block i >> 2,
 //           word i & 3: oracle/philox.py linear_words; not the segment map of philox_word);
-//   l_i   = floor(fl64(fl64(s * |g_i|) / norm) + U_i)   in [0, s]; 0 when not finite;
+//   l_i   = floor(fl64(|g_i| * c) + U_i)   in [0, s]; 0 when not finite; c = fl64(s / norm)
+//           (one fp64 multiply per element: the per-element fp64 division made the quantise
+//           pass VALU-bound, 176-183 us at 128 M);
 //   code  = signbit(g_i) << (W - 1) | l_i,  W = 4 (bits <= 2), 8 (<= 6), 16 (<= 14) bits,
 //           packed little-endian, 32 / W codes per uint32;
 //   value = (float)(+-(norm / (s * tau)) * l_i)   (fp64 product, one rounding to fp32).
@@ -23,12 +25,16 @@ namespace fc {
 
 constexpr int kQsgdNormGrid = 1024;            // fixed: the fp64 sum order depends on it
 constexpr int kQsgdElems = 8;                  // elements per thread per step (quant/decode)
+constexpr int kQsgdNormUnroll = 4;             // float4 loads in flight per thread (norm pass)
+// (Plain cache-allocating loads, so that a back-to-front quantise pass could re-read the norm
+// pass's tail from the Infinity Cache, measured slower: norm 98 -> 145 us at 128 M, and the
+// quantise no faster; profiles/r04_ab_qsgd.jsonl.)
 
 __host__ __device__ inline int qsgd_width(int bits) { return bits <= 2 ? 4 : bits <= 6 ? 8 : 16; }
 
 struct QsgdParams {                            // from the header (decode) or the encode args
   double norm, scale;                          // scale = norm / (s * tau)
-  double s;
+  double s, c;                                 // c = s / norm
   int width;
 };
 
@@ -46,8 +52,21 @@ __global__ __launch_bounds__(kBlock) void k_qsgd_norm(const float* __restrict__ 
   __shared__ uint32_t s_flag;
   const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
   double acc = 0.0;
-  const uint64_t n4 = n / 4;
-  for (uint64_t q = (uint64_t)blockIdx.x * kBlock + tid; q < n4; q += (uint64_t)gridDim.x * kBlock) {
+  const uint64_t n4 = n / 4, stride = (uint64_t)gridDim.x * kBlock;
+  // kQsgdNormUnroll float4 loads in flight per thread (one load per dependent fp64 chain step
+  // kept this pass latency-bound); the additions stay in the same per-thread order
+  uint64_t q = (uint64_t)blockIdx.x * kBlock + tid;
+  for (; q + (kQsgdNormUnroll - 1) * stride < n4; q += kQsgdNormUnroll * stride) {
+    float4 v[kQsgdNormUnroll];
+#pragma unroll
+    for (int u = 0; u < kQsgdNormUnroll; ++u) v[u] = load4_full(g + 4 * (q + u * stride));
+#pragma unroll
+    for (int u = 0; u < kQsgdNormUnroll; ++u) {
+      acc += (double)v[u].x * v[u].x; acc += (double)v[u].y * v[u].y;
+      acc += (double)v[u].z * v[u].z; acc += (double)v[u].w * v[u].w;
+    }
+  }
+  for (; q < n4; q += stride) {
     const float4 v = load4_full(g + 4 * q);
     acc += (double)v.x * v.x; acc += (double)v.y * v.y;
     acc += (double)v.z * v.z; acc += (double)v.w * v.w;
@@ -94,13 +113,14 @@ __device__ __forceinline__ QsgdParams qsgd_params(double norm, int bits, uint64_
   q.norm = norm;
   q.s = (double)(1u << bits);
   q.scale = norm / (q.s * qsgd_tau((double)n, q.s));
+  q.c = norm != 0.0 ? q.s / norm : __longlong_as_double(0x7ff0000000000000ll);
   q.width = qsgd_width(bits);
   return q;
 }
 
 __device__ __forceinline__ uint32_t qsgd_code(float x, uint32_t word, const QsgdParams& q) {
   const double u = (double)(word >> 8) * (1.0 / 16777216.0);
-  const double r = (q.s * (double)__builtin_fabsf(x)) / q.norm;
+  const double r = (double)__builtin_fabsf(x) * q.c;
   const double f = floor(r + u);
   const uint32_t l = (f >= 0.0 && f <= q.s) ? (uint32_t)f : 0u;   // NaN / inf -> 0
   return ((__float_as_uint(x) >> 31) << (q.width - 1)) | l;
@@ -117,8 +137,9 @@ __global__ __launch_bounds__(kBlock) void k_qsgd_quant(const float* __restrict__
                                                        const fc_packet_hdr* hdr, uint32_t* codes) {
   const QsgdParams q = qsgd_params(hdr->p, bits, n);
   const uint64_t groups = (n + kQsgdElems - 1) / kQsgdElems;
-  for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < groups;
-       t += (uint64_t)gridDim.x * kBlock) {
+  for (uint64_t t0 = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t0 < groups;
+       t0 += (uint64_t)gridDim.x * kBlock) {
+    const uint64_t t = t0;
     const uint64_t e = t * kQsgdElems;
     float x[8];
     if (e + 8 <= n) {
@@ -199,9 +220,10 @@ __global__ __launch_bounds__(kBlock) void k_qsgd_decode(QsgdDecodeArgs a) {
         acc[j] = ACC ? __fadd_rn(acc[j], __fmul_rn(d, v.weight)) : d;
       }
     }
-    if (e + 8 <= n) {
-      *reinterpret_cast<float4*>(a.out + e) = make_float4(acc[0], acc[1], acc[2], acc[3]);
-      *reinterpret_cast<float4*>(a.out + e + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
+    if (e + 8 <= n) {                            // non-temporal 16-B stores (dense output)
+      fc_f4v v0 = {acc[0], acc[1], acc[2], acc[3]}, v1 = {acc[4], acc[5], acc[6], acc[7]};
+      __builtin_nontemporal_store(v0, reinterpret_cast<fc_f4v*>(a.out + e));
+      __builtin_nontemporal_store(v1, reinterpret_cast<fc_f4v*>(a.out + e + 4));
     } else {
 #pragma unroll
       for (int j = 0; j < 8; ++j) if (e + j < n) a.out[e + j] = acc[j];

@@ -178,6 +178,14 @@ __device__ __forceinline__ void seg_lane(const SamplePlan& P, uint32_t s, int ti
   e = (uint32_t)st + (uint32_t)tid * 4u;
 }
 
+// gh[b] += h[b] for the non-empty bins of a 4096-bin LDS histogram (256 threads).  (Two bins
+// per 64-bit atomic measured SLOWER: +10 us per lone encode, the last arriver's shard loads
+// queued behind the 64-bit atomics, profiles/r04_ab_sample_chain.jsonl.)
+__device__ __forceinline__ void flush_hist(uint32_t* gh, const uint32_t* h) {
+  for (int b = threadIdx.x; b < kHistBins; b += kBlock)
+    if (h[b]) atomicAdd(&gh[b], h[b]);
+}
+
 // Sample loads: 4 consecutive elements of g as the float4 whose mag_key gives their keys.
 // float32: the values themselves.  float64 (fc_topk_dense_f64's sampled path, fc_f64.hip): the
 // 31-bit HIGH key of each double (|x| bits >> 32: exponent + 20 mantissa bits) as a float bit
@@ -346,11 +354,7 @@ __device__ __forceinline__ void sample_body(const T* __restrict__ g, const Sampl
   }
   __syncthreads();
   FC_TR(3);
-  {                                               // flush into this workgroup's shard
-    uint32_t* gh = W.hist1 + (bid % kSampleShards) * kHistBins;
-    for (int b = tid; b < kHistBins; b += kBlock)
-      if (h[b]) atomicAdd(&gh[b], h[b]);
-  }
+  flush_hist(W.hist1 + (bid % kSampleShards) * kHistBins, h);   // into this workgroup's shard
   FC_TR(4);
   if (!last_block_arrive_tree(W.tick, nb, bid, &sm.s_flag, 18)) return;
   FC_TR(5);
@@ -1192,11 +1196,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve(ResolveArgs a0) {
     });
     __syncthreads();
     FC_TR(29);
-    {                                                     // this workgroup's shard
-      uint32_t* gh = a.W.chist + (blockIdx.x % kCandShards) * kHistBins;
-      for (int b = tid; b < kHistBins; b += kBlock)
-        if (h[b]) atomicAdd(&gh[b], h[b]);
-    }
+    flush_hist(a.W.chist + (blockIdx.x % kCandShards) * kHistBins, h);   // this workgroup's shard
     FC_TR(27);
     if (last_block_arrive_tree(a.W.tick + 2 * kTickWords, gridDim.x, blockIdx.x, &s_flag)) {
       // the last arriver sums the shards (every load first, then the clearing stores: their

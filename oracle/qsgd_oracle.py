@@ -12,7 +12,7 @@ with respect to the reference.  This module states the exact arithmetic the HIP 
 (openmsftl_amd/csrc/fc_qsgd.hip) implements, so the GPU is pinned to it bit for bit:
 
     U_i   = (linear_word(i) >> 8) * 2**-24          (oracle/philox.py linear_words)
-    l_i   = floor(fl64(fl64(s * |g_i|) / norm) + U_i)   in [0, s];  0 if not finite
+    l_i   = floor(fl64(|g_i| * c) + U_i)   in [0, s];  0 if not finite,  c = fl64(s / norm)
     code  = signbit(g_i) << (W - 1) | l_i,  W = 4 / 8 / 16 bits for bits <= 2 / 6 / 14
     value = fl32(+-(norm / (s * tau)) * l_i)         (fp64 product, one rounding)
 
@@ -45,7 +45,8 @@ def levels_and_signs(g: np.ndarray, bits: int, seed: int, offset: int, norm: flo
     s = float(2 ** bits)
     u = (ph.linear_words(g.shape[0], seed, offset) >> np.uint32(8)).astype(np.float64) * 2.0 ** -24
     with np.errstate(invalid="ignore", divide="ignore", over="ignore"):
-        r = (s * np.abs(g.astype(np.float64))) / norm
+        c = s / norm if norm != 0.0 else math.inf            # fl64(s / norm), once
+        r = np.abs(g.astype(np.float64)) * c
         f = np.floor(r + u)
     ok = np.isfinite(f) & (f >= 0) & (f <= s)
     lev = np.where(ok, f, 0).astype(np.uint32)
