@@ -304,9 +304,14 @@ static uint32_t resolve_grid(uint32_t nchunks, uint32_t want) {
   return g > need ? g : need;
 }
 
+#ifndef FC_RESOLVE_CPW
+#define FC_RESOLVE_CPW 8          // lone encode: >= this many chunks per k_resolve workgroup
+#endif
 static int launch_resolve(const ResolveArgs& a, hipStream_t s) {
   TimedLaunch t(FC_TIME_ENGINE, s);
-  hipLaunchKernelGGL(k_resolve, dim3(resolve_grid(a.nchunks, kResolveGrid)), dim3(kBlock), 0, s, a);
+  const uint32_t want = std::max<uint32_t>(32u, std::min<uint32_t>((uint32_t)kResolveGrid,
+                                            (a.nchunks + FC_RESOLVE_CPW - 1) / FC_RESOLVE_CPW));
+  hipLaunchKernelGGL(k_resolve, dim3(resolve_grid(a.nchunks, want)), dim3(kBlock), 0, s, a);
   FC_LAUNCHED("k_resolve");
   return FC_OK;
 }
@@ -721,7 +726,7 @@ int fc_qsgd_decode(const fc_packet_view* pkt, uint64_t n, float* out, fc_stream_
   a.one = *pkt; a.m = 1; a.n = n; a.out = out;
   hipStream_t s = (hipStream_t)stream;
   TimedLaunch t(FC_TIME_DECODE, s);
-  hipLaunchKernelGGL(k_qsgd_decode<false>, dim3(stream_grid((n + kQsgdElems - 1) / kQsgdElems)), dim3(kBlock), 0, s, a);
+  hipLaunchKernelGGL(k_qsgd_decode<false>, dim3(stream_grid((n + 3) / 4)), dim3(kBlock), 0, s, a);
   FC_LAUNCHED("k_qsgd_decode");
   return FC_OK;
 }
@@ -737,7 +742,7 @@ int fc_qsgd_decode_accumulate(const fc_packet_view* views_dev, int m, uint64_t n
   a.views = views_dev; a.m = m; a.acc_in = continue_sum != 0; a.n = n; a.out = out;
   hipStream_t s = (hipStream_t)stream;
   TimedLaunch t(FC_TIME_DECODE, s);
-  hipLaunchKernelGGL(k_qsgd_decode<true>, dim3(stream_grid((n + kQsgdElems - 1) / kQsgdElems)), dim3(kBlock), 0, s, a);
+  hipLaunchKernelGGL(k_qsgd_decode<true>, dim3(stream_grid((n + 3) / 4)), dim3(kBlock), 0, s, a);
   FC_LAUNCHED("k_qsgd_decode(acc)");
   return FC_OK;
 }

@@ -10,11 +10,14 @@
 // E[q] = g / tau.)  Exact arithmetic of this build, shared with the oracle:
 //   norm  = sqrt(sum of g_i^2 in fp64), the sum in a fixed order (k_qsgd_norm), stored as a
 //           double in the header's `p` field;
-//   U_i   = (w_i >> 8) * 2^-24, w_i = Philox word i of the LINEAR map (counter block i >> 2,
-//           word i & 3: oracle/philox.py linear_words; not the segment map of philox_word);
-//   l_i   = floor(fl64(|g_i| * c) + U_i)   in [0, s]; 0 when not finite; c = fl64(s / norm)
-//           (one fp64 multiply per element: the per-element fp64 division made the quantise
-//           pass VALU-bound, 176-183 us at 128 M);
+//   U_i   = h_i * 2^-16, h_i = 16-bit half (i & 1) of Philox word (i >> 1) of the LINEAR map
+//           (counter block i >> 3: one Philox-4x32-10 block dithers 8 elements;
+//           oracle/philox.py linear_words; not the segment map of philox_word);
+//   l_i   = floor(fl32(fl32(|g_i| * c) + U_i))   in [0, s]; 0 when not finite;
+//           c = fl32(fl64(s / norm)); when that overflows (a norm below s / FLT_MAX) the same
+//           formula in fp64 with c = fl64(s / norm).  (The quantise pass was VALU-bound: a
+//           per-element fp64 division and two Philox blocks per 8 elements took 176-183 us at
+//           128 M; fp32 arithmetic and one block per 8 elements, see profiles/r04_*qsgd*);
 //   code  = signbit(g_i) << (W - 1) | l_i,  W = 4 (bits <= 2), 8 (<= 6), 16 (<= 14) bits,
 //           packed little-endian, 32 / W codes per uint32;
 //   value = (float)(+-(norm / (s * tau)) * l_i)   (fp64 product, one rounding to fp32).
@@ -35,6 +38,7 @@ __host__ __device__ inline int qsgd_width(int bits) { return bits <= 2 ? 4 : bit
 struct QsgdParams {                            // from the header (decode) or the encode args
   double norm, scale;                          // scale = norm / (s * tau)
   double s, c;                                 // c = s / norm
+  float s32, c32;                              // fl32 of both (c32 = +inf: use the fp64 form)
   int width;
 };
 
@@ -114,15 +118,25 @@ __device__ __forceinline__ QsgdParams qsgd_params(double norm, int bits, uint64_
   q.s = (double)(1u << bits);
   q.scale = norm / (q.s * qsgd_tau((double)n, q.s));
   q.c = norm != 0.0 ? q.s / norm : __longlong_as_double(0x7ff0000000000000ll);
+  q.s32 = (float)q.s;
+  q.c32 = (float)q.c;
   q.width = qsgd_width(bits);
   return q;
 }
 
-__device__ __forceinline__ uint32_t qsgd_code(float x, uint32_t word, const QsgdParams& q) {
-  const double u = (double)(word >> 8) * (1.0 / 16777216.0);
-  const double r = (double)__builtin_fabsf(x) * q.c;
-  const double f = floor(r + u);
-  const uint32_t l = (f >= 0.0 && f <= q.s) ? (uint32_t)f : 0u;   // NaN / inf -> 0
+// h: the element's 16 dither bits.  F32: c32 is finite (uniform per launch).
+template <bool F32>
+__device__ __forceinline__ uint32_t qsgd_code(float x, uint32_t h, const QsgdParams& q) {
+  uint32_t l;
+  if (F32) {
+    const float u = (float)h * (1.0f / 65536.0f);                // exact
+    const float f = floorf(__fadd_rn(__fmul_rn(__builtin_fabsf(x), q.c32), u));
+    l = (f >= 0.0f && f <= q.s32) ? (uint32_t)f : 0u;           // NaN / inf -> 0
+  } else {
+    const double u = (double)h * (1.0 / 65536.0);
+    const double f = floor((double)__builtin_fabsf(x) * q.c + u);
+    l = (f >= 0.0 && f <= q.s) ? (uint32_t)f : 0u;
+  }
   return ((__float_as_uint(x) >> 31) << (q.width - 1)) | l;
 }
 __device__ __forceinline__ float qsgd_value(uint32_t code, const QsgdParams& q) {
@@ -149,11 +163,15 @@ __global__ __launch_bounds__(kBlock) void k_qsgd_quant(const float* __restrict__
 #pragma unroll
       for (int j = 0; j < 8; ++j) x[j] = e + j < n ? g[e + j] : 0.f;
     }
-    const uint4 r0 = philox_block(e >> 2, seed, offset), r1 = philox_block((e >> 2) + 1, seed, offset);
-    const uint32_t wd[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+    const uint4 r0 = philox_block(e >> 3, seed, offset);       // 8 x 16 dither bits
+    const uint32_t wd[4] = {r0.x, r0.y, r0.z, r0.w};
     uint32_t c[8];
+    const bool f32 = q.c32 != __builtin_inff();
 #pragma unroll
-    for (int j = 0; j < 8; ++j) c[j] = e + j < n ? qsgd_code(x[j], wd[j], q) : 0u;
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t h = (wd[j >> 1] >> (16 * (j & 1))) & 0xffffu;
+      c[j] = e + j >= n ? 0u : f32 ? qsgd_code<true>(x[j], h, q) : qsgd_code<false>(x[j], h, q);
+    }
     if (q.width == 4) {
       uint32_t v = 0;
 #pragma unroll
@@ -178,55 +196,67 @@ struct QsgdDecodeArgs {
   float* out;
 };
 
-__device__ __forceinline__ void qsgd_unpack(const uint32_t* codes, uint64_t t, int width,
-                                            uint32_t (&c)[8]) {
-  typedef __attribute__((address_space(1))) const uint32_t gu;
+// The 4 codes of quad qd (elements 4 qd .. 4 qd + 3): 16 / 32 / 64 bits at quad index qd of
+// the packed words (W = 4 / 8 / 16; little-endian W-bit fields, so a quad is contiguous).
+__device__ __forceinline__ void qsgd_unpack4(const uint32_t* codes, uint64_t qd, int width,
+                                             uint32_t (&c)[4]) {
   if (width == 4) {
-    const uint32_t v = ((gu*)codes)[t];
+    typedef __attribute__((address_space(1))) const uint16_t gu16;
+    const uint32_t v = ((gu16*)codes)[qd];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) c[j] = (v >> (4 * j)) & 0xfu;
+    for (int j = 0; j < 4; ++j) c[j] = (v >> (4 * j)) & 0xfu;
   } else if (width == 8) {
-    typedef __attribute__((address_space(1))) const fc_u32x2 gu2;
-    const fc_u32x2 v = ((gu2*)codes)[t];
+    typedef __attribute__((address_space(1))) const uint32_t gu;
+    const uint32_t v = ((gu*)codes)[qd];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) { c[j] = (v.x >> (8 * j)) & 0xffu; c[4 + j] = (v.y >> (8 * j)) & 0xffu; }
+    for (int j = 0; j < 4; ++j) c[j] = (v >> (8 * j)) & 0xffu;
   } else {
-    typedef __attribute__((address_space(1))) const fc_u32x4 gu4;
-    const fc_u32x4 v = ((gu4*)codes)[t];
+    typedef __attribute__((address_space(1))) const fc_u32x2 gu2;
+    const fc_u32x2 v = ((gu2*)codes)[qd];
     c[0] = v.x & 0xffffu; c[1] = v.x >> 16; c[2] = v.y & 0xffffu; c[3] = v.y >> 16;
-    c[4] = v.z & 0xffffu; c[5] = v.z >> 16; c[6] = v.w & 0xffffu; c[7] = v.w >> 16;
   }
 }
 
+// Thread = one quad of 4 elements: its codes are one 2 / 4 / 8-B load and its 4 values one
+// 16-B store, so every store instruction writes a contiguous 1 KB per wave.  (8 elements per
+// thread wrote two 16-B halves 32 B apart per lane: 146 us per 128 M decode with plain stores,
+// 239 us with non-temporal ones, which do not merge the halves.)
 template <bool ACC>
 __global__ __launch_bounds__(kBlock) void k_qsgd_decode(QsgdDecodeArgs a) {
-  const uint64_t n = a.n, groups = (n + kQsgdElems - 1) / kQsgdElems;
+  const uint64_t n = a.n, quads = (n + 3) / 4;
   const int M = ACC ? a.m : 1;
-  for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < groups;
-       t += (uint64_t)gridDim.x * kBlock) {
-    const uint64_t e = t * kQsgdElems;
-    float acc[8];
+  for (uint64_t qd = (uint64_t)blockIdx.x * kBlock + threadIdx.x; qd < quads;
+       qd += (uint64_t)gridDim.x * kBlock) {
+    const uint64_t e = qd * 4;
+    const bool full = e + 4 <= n;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    if (ACC && a.acc_in) {
+      if (full) {
+        const fc_f4v v = *(fc_gf4v*)(a.out + e);
+        acc[0] = v.x; acc[1] = v.y; acc[2] = v.z; acc[3] = v.w;
+      } else {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] = (ACC && a.acc_in && e + j < n) ? a.out[e + j] : 0.f;
+        for (int j = 0; j < 4; ++j) if (e + j < n) acc[j] = a.out[e + j];
+      }
+    }
     for (int m = 0; m < M; ++m) {                                // rows in order (gar.py:44)
       const fc_packet_view& v = ACC ? a.views[m] : a.one;
       const fc_packet_hdr* h = v.hdr;
       const QsgdParams q = qsgd_params(h->p, (int)h->k, n);
-      uint32_t c[8];
-      qsgd_unpack(static_cast<const uint32_t*>(v.idx), t, q.width, c);
+      uint32_t c[4];
+      qsgd_unpack4(static_cast<const uint32_t*>(v.idx), qd, q.width, c);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
+      for (int j = 0; j < 4; ++j) {
         const float d = qsgd_value(c[j], q);
         acc[j] = ACC ? __fadd_rn(acc[j], __fmul_rn(d, v.weight)) : d;
       }
     }
-    if (e + 8 <= n) {                            // non-temporal 16-B stores (dense output)
-      fc_f4v v0 = {acc[0], acc[1], acc[2], acc[3]}, v1 = {acc[4], acc[5], acc[6], acc[7]};
-      __builtin_nontemporal_store(v0, reinterpret_cast<fc_f4v*>(a.out + e));
-      __builtin_nontemporal_store(v1, reinterpret_cast<fc_f4v*>(a.out + e + 4));
+    if (full) {
+      __builtin_nontemporal_store(fc_f4v{acc[0], acc[1], acc[2], acc[3]},
+                                  reinterpret_cast<fc_f4v*>(a.out + e));
     } else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) if (e + j < n) a.out[e + j] = acc[j];
+      for (int j = 0; j < 4; ++j) if (e + j < n) a.out[e + j] = acc[j];
     }
   }
 }

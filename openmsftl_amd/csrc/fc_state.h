@@ -16,8 +16,9 @@ struct alignas(16) TopkState {
   uint64_t e_prefix;     // exact radix engine: resolved high bits of T64
   uint32_t err;          // sticky device error (spin timeout)
   uint32_t a_done, b_done, r_done;
-  uint32_t win_klo, win_khi, win_fs;   // k_sample1's fine window, published by workgroup 0
-  uint32_t win_flag;     // 1 once the window is published; reset by the sample's last block
+  uint32_t pad0_[3];
+  uint32_t win_flag;     // k_sample1's fine window, published by workgroup 0: bit 31 valid,
+                         // level-1 bins hi << 12 | lo; reset by the sample's last block
   uint32_t pad1_[2];
   uint32_t t_lo, t_hi;   // bracket (keys): list key >= t_lo; candidates key <= t_hi
   uint32_t sbin;         // candidate histogram bin = (key - t_lo) >> sbin  (< 4096 bins)

@@ -169,6 +169,16 @@ __device__ __forceinline__ uint32_t fine_upper(uint32_t b, const FineWin& F) {
   return u > 0xffffffffull ? 0xffffffffu : (uint32_t)u;
 }
 
+// The fine window spanning level-1 (key >> 19) bins blo .. bhi.
+__device__ __forceinline__ FineWin win_of(uint32_t blo, uint32_t bhi) {
+  FineWin F;
+  F.klo = blo << 19;
+  F.khi = ((bhi + 1u) << 19) - 1u;
+  F.fs = 0;
+  while (((F.khi - F.klo) >> F.fs) >= kFineBins) ++F.fs;
+  return F;
+}
+
 // Segment s of the sample: element range [e, lim) of this thread's float4.
 // (n < 2^32: 32-bit bounds keep k_fused_mag's sample part inside 64 VGPRs)
 __device__ __forceinline__ void seg_lane(const SamplePlan& P, uint32_t s, int tid, uint32_t& e,
@@ -178,6 +188,12 @@ __device__ __forceinline__ void seg_lane(const SamplePlan& P, uint32_t s, int ti
   e = (uint32_t)st + (uint32_t)tid * 4u;
 }
 
+#ifndef FC_PKT_DIRECT
+#define FC_PKT_DIRECT 0       // 1: packet entries straight to the slot, no LDS stage (A/B)
+#endif
+#ifndef FC_SHARDS_ADAPT
+#define FC_SHARDS_ADAPT 1
+#endif
 // gh[b] += h[b] for the non-empty bins of a 4096-bin LDS histogram (256 threads).  (Two bins
 // per 64-bit atomic measured SLOWER: +10 us per lone encode, the last arriver's shard loads
 // queued behind the 64-bit atomics, profiles/r04_ab_sample_chain.jsonl.)
@@ -252,12 +268,7 @@ __device__ __forceinline__ FineWin pilot_window(const T* __restrict__ g, const S
   FC_TR(21);
   find_ranks_desc(h, (uint32_t)P.pr_hi, (uint32_t)P.pr_lo, s_tmp, s_out);
   FC_TR(22);
-  FineWin F;
-  F.klo = s_out[2] << 19;
-  F.khi = ((s_out[0] + 1u) << 19) - 1u;
-  F.fs = 0;
-  while (((F.khi - F.klo) >> F.fs) >= kFineBins) ++F.fs;
-  return F;
+  return win_of(s_out[2], s_out[0]);
 }
 
 // One launch: grid (ceil(nseg / kSampleSegs), clients).  A lone client's launch (<= 256
@@ -315,22 +326,21 @@ __device__ __forceinline__ void sample_body(const T* __restrict__ g, const Sampl
   if (SHARED_ONLY) shared_pilot = true;
   if (!shared_pilot || bid == 0) {
     F = pilot_window<KM, SHARED_ONLY, T>(g, P, seed, off, h, s_tmp, s_out, bid == 0, xs, es, ls);
-    if (shared_pilot && tid == 0) {               // publish: sc1 payload, drained, sc1 flag
-      st_agent(&S->win_klo, F.klo); st_agent(&S->win_khi, F.khi); st_agent(&S->win_fs, F.fs);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      st_agent(&S->win_flag, 1u);
-    }
+    // publish the window as ONE sc1 word (its two level-1 bins, bit 31 = valid): the pollers'
+    // load returns the payload itself (a flag then three payload loads was one more round trip)
+    if (shared_pilot && tid == 0)
+      st_agent(&S->win_flag, 0x80000000u | ((F.khi >> 19) << 12) | (F.klo >> 19));
     for (int b = tid; b < kHistBins; b += kBlock) h[b] = 0;   // find_ranks_desc ended on a barrier
   } else {
-    if (tid == 0) {                               // relaxed sc1 poll (bounded), sc1 payload
-      uint32_t it = 0;
-      while (ld_agent(&S->win_flag) == 0u && ++it < kSpinMax) __builtin_amdgcn_s_sleep(2);
-      s_win[0] = ld_agent(&S->win_klo); s_win[1] = ld_agent(&S->win_khi);
-      s_win[2] = it < kSpinMax ? ld_agent(&S->win_fs) : 0xffu;   // timeout: poisoned
+    if (tid == 0) {                               // relaxed sc1 poll (bounded) of the payload
+      uint32_t it = 0, w;
+      while (((w = ld_agent(&S->win_flag)) >> 31) == 0u && ++it < kSpinMax) __builtin_amdgcn_s_sleep(2);
+      s_win[0] = w;
     }
     __syncthreads();
-    F.klo = s_win[0]; F.khi = s_win[1]; F.fs = s_win[2];
-    if (F.fs == 0xffu) {                          // never expected: make the resolve retry
+    const uint32_t w = s_win[0];
+    F = win_of(w & 0xfffu, (w >> 12) & 0xfffu);
+    if ((w >> 31) == 0u) {                        // timed out (never expected): make the resolve retry
       if (tid == 0) st_agent(&S->err, 1u);
       F.klo = 0; F.khi = 0xffffffffu; F.fs = 31;
     }
@@ -354,7 +364,10 @@ __device__ __forceinline__ void sample_body(const T* __restrict__ g, const Sampl
   }
   __syncthreads();
   FC_TR(3);
-  flush_hist(W.hist1 + (bid % kSampleShards) * kHistBins, h);   // into this workgroup's shard
+  // histogram shards: one per 32 workgroups (<= kSampleShards): a small launch's last arriver
+  // then sums fewer shards (a lone 16 M encode has 128 sample workgroups)
+  const uint32_t nsh = FC_SHARDS_ADAPT ? min((uint32_t)kSampleShards, max(1u, nb / 32u)) : (uint32_t)kSampleShards;
+  flush_hist(W.hist1 + (bid % nsh) * kHistBins, h);   // into this workgroup's shard
   FC_TR(4);
   if (!last_block_arrive_tree(W.tick, nb, bid, &sm.s_flag, 18)) return;
   FC_TR(5);
@@ -368,6 +381,7 @@ __device__ __forceinline__ void sample_body(const T* __restrict__ g, const Sampl
     for (int j = 0; j < kPer; ++j) t[j] = 0;
 #pragma unroll
     for (int sh = 0; sh < kSampleShards; ++sh)
+      if ((uint32_t)sh < nsh)
 #pragma unroll
       for (int j = 0; j < kPer; ++j) t[j] += ld_agent(&W.hist1[sh * kHistBins + j * kBlock + tid]);
 #pragma unroll
@@ -404,7 +418,7 @@ __device__ __forceinline__ void sample_body(const T* __restrict__ g, const Sampl
   }
   // clear the shards for the next call last, with plain 16-B stores (their next use is an
   // atomic in the next launch, after this kernel's end-of-launch write-back)
-  for (int i = tid; i < kHistBins * kSampleShards / 4; i += kBlock)
+  for (uint32_t i = tid; i < (uint32_t)kHistBins * nsh / 4; i += kBlock)
     reinterpret_cast<uint4*>(W.hist1)[i] = make_uint4(0u, 0u, 0u, 0u);
   FC_TR(6);
 }
@@ -651,7 +665,7 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
   if (!PKT) {                                           // dense only: q, no entries
 #pragma unroll
     for (int q = 0; q < NQ; ++q) dense_out(q, mag_listed<FAST>(P, x[q]));
-  } else if (tot_e <= (uint32_t)SH::kStageN) {          // block-uniform
+  } else if (!FC_PKT_DIRECT && tot_e <= (uint32_t)SH::kStageN) {   // block-uniform
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const bool p = mag_listed<FAST>(P, x[q]);
@@ -712,7 +726,7 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
     if (tot_c) atomicAdd(&S->shard_cnd[chunk % kShards], tot_c);
   }
   if (!PKT && c_ovf) direct_entries(false);            // rare: the resolve reads them
-  if (PKT && tot_e <= (uint32_t)SH::kStageN) {          // coalesced 16-B stores of the staged slot
+  if (PKT && !FC_PKT_DIRECT && tot_e <= (uint32_t)SH::kStageN) {   // coalesced 16-B stores of the staged slot
     for (uint32_t t = 4 * tid; t < tot_e; t += 4 * MagGeo<NW>::kThreads) {
       if (t + 4 <= tot_e) {
         const uint4 p0 = *reinterpret_cast<const uint4*>(&sh.st[t]);
@@ -1012,6 +1026,16 @@ __device__ __forceinline__ void fused_mag_wg(const CompactArgs& a0, const Sample
   const MagState st = s_st;
   constexpr bool kBin = DENSE ? FC_FUSED_BIN_DENSE != 0 : FC_FUSED_BIN_PKT != 0;
   compact_mag_item<NW, MagShared, DENSE, kBin, !DENSE || FC_DENSE_PKT != 0>(a0, mag_out(a0, 0u), chunk, st, x, u.m);
+#ifdef FC_ABL_DRAIN
+  // ablation (A/B only): what an in-kernel completion count would cost every chunk workgroup —
+  // drain its stores (1), plus one atomic on one of 64 group counters (2)
+  if (DENSE) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (FC_ABL_DRAIN == 2 && threadIdx.x == 0)
+      atomicAdd(reinterpret_cast<uint32_t*>(a0.W.small) + (chunk % 64) * 64, 1u);
+  }
+#endif
   FC_TR(26);
 }
 template <bool DENSE>

@@ -71,7 +71,8 @@ def element_words(n: int, seed: int, offset: int = 0, start: int = 0) -> np.ndar
 
 
 def linear_words(n: int, seed: int, offset: int = 0, start: int = 0) -> np.ndarray:
-    """QSGD's dither words: block i >> 2, word i & 3 (fc_qsgd.hip)."""
+    """Linear word map: word i = word i & 3 of counter block i >> 2.  QSGD dithers element e
+    with the 16-bit half (e & 1) of word e >> 1 (fc_qsgd.hip, oracle/qsgd_oracle.py)."""
     if n == 0:
         return np.zeros(0, dtype=np.uint32)
     idx = np.arange(start, start + n, dtype=np.uint64)

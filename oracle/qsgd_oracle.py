@@ -11,8 +11,10 @@ encoding", NeurIPS 2017).  There is no reference output to pin against: **parity
 with respect to the reference.  This module states the exact arithmetic the HIP codec
 (openmsftl_amd/csrc/fc_qsgd.hip) implements, so the GPU is pinned to it bit for bit:
 
-    U_i   = (linear_word(i) >> 8) * 2**-24          (oracle/philox.py linear_words)
-    l_i   = floor(fl64(|g_i| * c) + U_i)   in [0, s];  0 if not finite,  c = fl64(s / norm)
+    U_i   = h_i * 2**-16,  h_i = 16-bit half (i & 1) of linear word (i >> 1)
+            (oracle/philox.py linear_words: one Philox block per 8 elements)
+    l_i   = floor(fl32(fl32(|g_i| * c) + U_i))   in [0, s];  0 if not finite,
+            c = fl32(fl64(s / norm));  if that overflows, the same in fp64 with c = fl64(s / norm)
     code  = signbit(g_i) << (W - 1) | l_i,  W = 4 / 8 / 16 bits for bits <= 2 / 6 / 14
     value = fl32(+-(norm / (s * tau)) * l_i)         (fp64 product, one rounding)
 
@@ -43,11 +45,18 @@ def norm64(g: np.ndarray) -> float:
 
 def levels_and_signs(g: np.ndarray, bits: int, seed: int, offset: int, norm: float):
     s = float(2 ** bits)
-    u = (ph.linear_words(g.shape[0], seed, offset) >> np.uint32(8)).astype(np.float64) * 2.0 ** -24
+    n = g.shape[0]
+    w = ph.linear_words((n + 1) // 2, seed, offset)
+    h = (w[np.arange(n) >> 1] >> ((np.arange(n) & 1) * 16).astype(np.uint32)) & np.uint32(0xFFFF)
     with np.errstate(invalid="ignore", divide="ignore", over="ignore"):
         c = s / norm if norm != 0.0 else math.inf            # fl64(s / norm), once
-        r = np.abs(g.astype(np.float64)) * c
-        f = np.floor(r + u)
+        c32 = np.float32(c)
+        if np.isfinite(c32):                                 # fp32 arithmetic
+            u = h.astype(np.float32) * np.float32(2.0 ** -16)
+            f = np.floor(np.abs(g.astype(np.float32)) * c32 + u)
+        else:                                                # s / norm above FLT_MAX
+            u = h.astype(np.float64) * 2.0 ** -16
+            f = np.floor(np.abs(g.astype(np.float64)) * c + u)
     ok = np.isfinite(f) & (f >= 0) & (f <= s)
     lev = np.where(ok, f, 0).astype(np.uint32)
     sign = np.signbit(g).astype(np.uint32)
