@@ -54,7 +54,6 @@ static WsPtrs ws_ptrs(void* ws, uint64_t n) {
   W.ccnt = reinterpret_cast<uint32_t*>(b + L.off_status);
   W.cand = reinterpret_cast<uint64_t*>(b + L.off_cand);
   W.cand_cap = L.cand_cap;
-  W.tgrp = reinterpret_cast<uint32_t*>(b + L.off_tgrp);
   return W;
 }
 
@@ -465,8 +464,6 @@ int fc_topk_encode_dense(const float* g, uint64_t n, uint64_t k, uint16_t* idx, 
   if (fused_enabled()) {
     rc = launch_fused(ca, P, hi, sgrid, s);
     if (rc) return rc;
-    // the fused launch resolved T64 and wrote the candidates itself (FC_DENSE_TAIL, fc_topk.hip)
-    if (FC_DENSE_TAIL && !FC_DENSE_PKT) return FC_OK;
     ra.rbin = FC_FUSED_BIN_DENSE ? 0u : 1u;
   } else {
     ra.rbin = 1;

@@ -30,8 +30,7 @@ struct alignas(16) TopkState {
   uint32_t fz_seq;       // k_fused_mag launches completed (bumped by the following k_resolve)
   uint32_t hgen;         // k_resolve: bumped once the bin beta below is published
   uint32_t rb_beta, rb_rin, rb_cnt;   // k_resolve: bin holding rank r, rank inside it, its count
-  uint32_t tail_top;     // k_fused_mag<true> in-kernel resolve: completed chunk groups
-  uint32_t pad_[2];
+  uint32_t pad_[3];
   uint32_t shard_ent[kShards];   // k_compact totals, 64-way sharded (no hot word)
   uint32_t shard_cnd[kShards];
 };
@@ -48,11 +47,10 @@ constexpr int kCandShards = FC_CAND_SHARDS;       // k_resolve's candidate histo
 constexpr int kTickGroups = 16;             // two-level last-arriver tickets (fc_common.h)
 constexpr int kTickStride = 64;             // u32 per ticket counter (one 256-B line each)
 constexpr int kTickWords = (kTickGroups + 1) * kTickStride;
-constexpr int kTailGroups = 256;            // k_fused_mag<true>: chunk completion groups = resolvers
 
 struct WsLayout {
   uint64_t nchunks, cand_cap;
-  uint64_t off_hist1, off_tick, off_ehist, off_chist, off_small, off_status, off_cand, off_tgrp, bytes;
+  uint64_t off_hist1, off_tick, off_ehist, off_chist, off_small, off_status, off_cand, bytes;
   __host__ __device__ static WsLayout of(uint64_t n) {
     WsLayout L;
     L.nchunks = (n + kChunk - 1) / kChunk;
@@ -63,9 +61,6 @@ struct WsLayout {
     L.off_ehist = o;  o += 4ull * kHistBins;
     L.off_chist = o;  o += 4ull * kHistBins * kCandShards;
     L.off_small = o;  o += 8ull * kSmallCap;
-    // (self-cleaning counters sit before the n-sized regions: a workspace made for a larger n is
-    // reused for smaller ones, so their offsets must not depend on n)
-    L.off_tgrp = o;   o += 4ull * kTailGroups * kTickStride;   // completion counters, 256 B apart
     L.off_status = o; o += 4ull * (L.nchunks ? L.nchunks : 1);   // per-chunk candidate counts
     o = (o + 15) & ~15ull;
     L.off_cand = o;   o += 8ull * L.cand_cap;
@@ -87,7 +82,6 @@ struct WsPtrs {
   uint32_t* ccnt;          // candidates per chunk (may exceed kCandSlot: overflowed chunk)
   uint64_t* cand;          // chunk c's candidates at [c * kCandSlot, + min(ccnt, kCandSlot))
   uint64_t cand_cap;
-  uint32_t* tgrp;          // kTailGroups completion counters (kTickStride words apart)
 };
 
 // Batched encode: client j's workspace starts j * ws_stride bytes after client 0's.
@@ -100,7 +94,6 @@ __device__ __forceinline__ WsPtrs ws_shift(WsPtrs W, uint64_t bytes) {
   W.small = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(W.small) + bytes);
   W.ccnt = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(W.ccnt) + bytes);
   W.cand = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(W.cand) + bytes);
-  W.tgrp = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(W.tgrp) + bytes);
   return W;
 }
 

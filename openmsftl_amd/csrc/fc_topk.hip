@@ -105,13 +105,11 @@ __device__ void find_ranks_desc(const uint32_t* h, uint32_t r1, uint32_t r2, uin
   __syncthreads();
 }
 
-// Descending bitonic sort of P2 (power of two) uint64 values in LDS by the first nthr threads
-// (default: the whole workgroup; k_fused_mag's resolvers run 256 of their 512).
-__device__ void bitonic_desc(uint64_t* sv, uint32_t P2, uint32_t nthr = 0) {
-  const uint32_t nt = nthr ? nthr : blockDim.x;
+// Descending bitonic sort of P2 (power of two) uint64 values in LDS (256 threads).
+__device__ void bitonic_desc(uint64_t* sv, uint32_t P2) {
   for (uint32_t size = 2; size <= P2; size <<= 1) {
     for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
-      for (uint32_t t = threadIdx.x; t < P2 / 2; t += nt) {
+      for (uint32_t t = threadIdx.x; t < P2 / 2; t += blockDim.x) {
         const uint32_t i = 2 * t - (t & (stride - 1)), j = i + stride;
         const bool desc = (i & size) == 0;
         const uint64_t x = sv[i], y = sv[j];
@@ -293,7 +291,7 @@ __device__ __forceinline__ void sample_body(const T* __restrict__ g, const Sampl
                                             uint64_t seed, uint64_t off, const WsPtrs& W,
                                             uint32_t ib, fc_packet_hdr* hdr, const HdrInit& HI,
                                             uint32_t bid, uint32_t nb, bool shared_pilot,
-                                            SampleShared& sm, uint32_t pub, bool write_hdr = true) {
+                                            SampleShared& sm, uint32_t pub) {
   uint32_t* h = sm.h;
   uint32_t* s_tmp = sm.s_tmp;
   uint32_t* s_out = sm.s_out;
@@ -414,12 +412,9 @@ __device__ __forceinline__ void sample_body(const T* __restrict__ g, const Sampl
     }
     // the header's only writer in this launch: a static header written by workgroup 0 at its
     // start raced this store through another XCD's L2 (lower read back as 0).  Nothing in this
-    // launch reads it (k_resolve does, after the kernel boundary).  (!write_hdr: the fused
-    // dense launch's resolving workgroups write the whole header instead.)
-    if (write_hdr) {
-      write_hdr_static(hdr, HI);
-      hdr->lower = (uint64_t)t_lo << ib;
-    }
+    // launch reads it (k_resolve does, after the kernel boundary).
+    write_hdr_static(hdr, HI);
+    hdr->lower = (uint64_t)t_lo << ib;
   }
   // clear the shards for the next call last, with plain 16-B stores (their next use is an
   // atomic in the next launch, after this kernel's end-of-launch write-back)
@@ -591,13 +586,7 @@ struct MagOut {
 // PKT = false (the drop-in dense path, fc_topk_encode_dense): q is the product, the packet
 // entries are not written (-6 B per listed element of HBM writes) except for a chunk whose
 // candidates overflowed their slot (k_resolve re-reads that chunk's entries).
-// TAIL (fc_topk_encode_dense with the in-kernel resolve, k_fused_mag<true>): q is written for
-// every element EXCEPT the bracket's candidates (the resolving workgroups of the same launch
-// write those: byte-disjoint from these stores, so the order in which the XCDs' L2s write back
-// cannot matter); the candidates leave with their sign in bit 63 of the slot entry; the
-// candidate slot and count are sc1 stores, drained before the q stores are issued, so the
-// completion ticket taken after this body orders them for the resolving workgroups.
-template <bool FAST, typename SH, int NW, bool DENSE, bool BIN, bool PKT = true, bool TAIL = false>
+template <bool FAST, typename SH, int NW, bool DENSE, bool BIN, bool PKT = true>
 __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred& P,
                                                  float (&x)[MagGeo<NW>::kQ], SH& sh,
                                                  uint32_t chunk, uint32_t sbin) {
@@ -674,10 +663,8 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
     }
   };
   if (!PKT) {                                           // dense only: q, no entries
-    if (!TAIL) {
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) dense_out(q, mag_listed<FAST>(P, x[q]));
-    }
+    for (int q = 0; q < NQ; ++q) dense_out(q, mag_listed<FAST>(P, x[q]));
   } else if (!FC_PKT_DIRECT && tot_e <= (uint32_t)SH::kStageN) {   // block-uniform
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
@@ -707,11 +694,8 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
       const uint32_t pos = wc + prefix_count(mc);
       if (c) {
         const uint32_t e = base + FC_LOC(q);
-        const float gv = FAST ? x[q] : a.g[e];
-        const uint32_t key = mag_key(gv);
-        if (pos < (uint32_t)kCW)
-          sh.cst[w * kCW + pos] = comp_of(key, e, a.ib) |
-                                  (TAIL ? (uint64_t)(__float_as_uint(gv) >> 31) << 63 : 0ull);
+        const uint32_t key = mag_key(FAST ? x[q] : a.g[e]);
+        if (pos < (uint32_t)kCW) sh.cst[w * kCW + pos] = comp_of(key, e, a.ib);
         if (BIN) {
           const uint32_t bin = (key - P.t_lo) >> sbin;
           if (pos < (uint32_t)kCW) sh.cstb[w * kCW + pos] = (uint16_t)bin;
@@ -734,19 +718,14 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
   }
   if (tid == 0) {
     TopkState* S = a.S;
+    a.cnt[chunk] = tot_e;
+    if (a.qoff) a.qoff[chunk] = qs1 | ((uint64_t)qs2 << 16) | ((uint64_t)qs3 << 32) | ((uint64_t)tot_e << 48);
     // a wave past its sub-slot: report more than the slot holds (k_resolve's overflow test)
-    const uint32_t cc = c_ovf ? max(tot_c, (uint32_t)kCandSlot + 1u) : tot_c;
-    if (TAIL) {
-      st_agent(&a.ccnt[chunk], cc);
-    } else {
-      a.cnt[chunk] = tot_e;
-      if (a.qoff) a.qoff[chunk] = qs1 | ((uint64_t)qs2 << 16) | ((uint64_t)qs3 << 32) | ((uint64_t)tot_e << 48);
-      a.ccnt[chunk] = cc;
-    }
+    a.ccnt[chunk] = c_ovf ? max(tot_c, (uint32_t)kCandSlot + 1u) : tot_c;
     atomicAdd(&S->shard_ent[chunk % kShards], tot_e);
     if (tot_c) atomicAdd(&S->shard_cnd[chunk % kShards], tot_c);
   }
-  if (!PKT && !TAIL && c_ovf) direct_entries(false);   // rare: the resolve reads them
+  if (!PKT && c_ovf) direct_entries(false);            // rare: the resolve reads them
   if (PKT && !FC_PKT_DIRECT && tot_e <= (uint32_t)SH::kStageN) {   // coalesced 16-B stores of the staged slot
     for (uint32_t t = 4 * tid; t < tot_e; t += 4 * MagGeo<NW>::kThreads) {
       if (t + 4 <= tot_e) {
@@ -776,21 +755,7 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
     }
     if (p < nj) {
       if (BIN) atomicAdd(&a.chist[sh.cstb[tid]], 1u);
-      if (!c_ovf) {
-        if (TAIL) st_agent(&a.cand[(uint64_t)chunk * kCandSlot + pre + p], sh.cst[tid]);
-        else a.cand[(uint64_t)chunk * kCandSlot + pre + p] = sh.cst[tid];
-      }
-    }
-  }
-  if (TAIL) {
-    // the slot, its count and the totals / histogram atomics drained (the loads of g are long
-    // done); then q for everything but the candidates, left in flight
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const bool p = mag_listed<FAST>(P, x[q]);
-      const bool c = P.cand_on && mag_cand<FAST>(P, x[q]);
-      if (!c) dense_out(q, p);
+      if (!c_ovf) a.cand[(uint64_t)chunk * kCandSlot + pre + p] = sh.cst[tid];
     }
   }
 }
@@ -901,7 +866,7 @@ __device__ __forceinline__ void mag_load(const float* g, uint32_t chunk, uint64_
 // workgroups per CU overlap one another's load latency.  (A persistent variant that kept the
 // next item's loads in flight measured 1.3-2.5x SLOWER: hipcc spilled the second register set
 // and loop-carried state)
-template <int NW, typename SH, bool DENSE, bool BIN, bool PKT = true, bool TAIL = false>
+template <int NW, typename SH, bool DENSE, bool BIN, bool PKT = true>
 __device__ __forceinline__ void compact_mag_item(const CompactArgs& a0, const MagOut& o,
                                                  uint32_t chunk, const MagState& st,
                                                  float (&x)[MagGeo<NW>::kQ], SH& sh) {
@@ -923,7 +888,7 @@ __device__ __forceinline__ void compact_mag_item(const CompactArgs& a0, const Ma
   P.cand_all = P.t_hi >= 0x7f800001u;
   P.T_hi = __uint_as_float(P.cand_all ? 0x7f800000u : P.t_hi);
   if (fast) {
-    compact_mag_body<true, SH, NW, DENSE, BIN, PKT, TAIL>(o, P, x, sh, chunk, st.sbin);
+    compact_mag_body<true, SH, NW, DENSE, BIN, PKT>(o, P, x, sh, chunk, st.sbin);
   } else if (none) {                                       // k = 0: nothing listed
     SH::barrier();
     if (tid == 0) {
@@ -936,7 +901,7 @@ __device__ __forceinline__ void compact_mag_item(const CompactArgs& a0, const Ma
         o.dense[base + i] = 0.0f;
   } else {                                                 // rare: exact integer predicate
     mag_exact_bits<NW>(P, x, base + (uint32_t)((tid >> 6) * 256 + lane_id()));
-    compact_mag_body<false, SH, NW, DENSE, BIN, PKT, TAIL>(o, P, x, sh, chunk, st.sbin);
+    compact_mag_body<false, SH, NW, DENSE, BIN, PKT>(o, P, x, sh, chunk, st.sbin);
   }
 }
 
@@ -1012,206 +977,10 @@ __global__ __launch_bounds__(kCBlock, FC_MAG1_WAVES_PER_EU) void k_compact_mag1_
 #ifndef FC_FZ_SLEEP
 #define FC_FZ_SLEEP 4         // s_sleep argument of the chunk workgroups' bracket poll
 #endif
-// ---- the in-kernel resolve of k_fused_mag<true> (FC_DENSE_TAIL) ---------------------------
-// The chunk workgroups count themselves complete in kTailGroups group counters (chunk c in
-// group c % G); the workgroup that completes a group becomes a RESOLVER (G of them, all of them
-// resident: they appear in the last round of chunks, and wait only for chunks that are running
-// or will get one of the >= 768 other slots).  The resolvers do k_resolve's work for the dense
-// path without a kernel boundary: the candidate histogram (binned by the chunks) -> bin beta of
-// rank k - #definite -> every resolver writes its chunks' candidates above beta (their value,
-// rebuilt from the slot entry: key | sign) or below it (+0) and gathers those in beta -> the
-// last one to arrive publishes "gathered" -> each picks T64 from the same <= 4096-entry list
-// and writes its beta candidates.  The chunks never wrote the candidates' q bytes, so no
-// ordering between the XCDs' L2 write-backs is needed; everything the resolvers read was
-// stored sc1 (or by device atomics) and drained before the chunk's completion ticket.
-#ifndef FC_DENSE_TAIL
-#define FC_DENSE_TAIL 1
-#endif
-constexpr int kTailMine = 512;                 // a resolver's own bin-beta candidates kept in LDS
-struct TailShared {
-  union {
-    uint32_t h[kHistBins];                     // candidate histogram, then ...
-    uint64_t sv[kSmallCap];                    // ... the gathered bin (rank count / sort)
-  };
-  uint64_t mine[kTailMine];
-  uint32_t s_tmp[8], s_out[4], s_flag, s_cnt, s_base, s_nmine, s_st, s_tot[2];
-  uint64_t s_T;
-};
 union FusedShared {
   SampleShared s;
   MagShared m;
-  TailShared t;
 };
-
-// fn(v) for every candidate of chunks [c0, c1): v = comp | sign << 63 from the chunk's slot
-// (sc1 loads), or rebuilt from g for a chunk whose candidates overflowed the slot.
-template <typename F>
-__device__ __forceinline__ void tail_cands(const CompactArgs& a, uint32_t c0, uint32_t c1,
-                                           uint32_t t_lo, uint32_t t_hi, F&& fn) {
-  constexpr uint32_t tpc = 16, cpr = kBlock / tpc;
-  for (uint32_t cb = c0; cb < c1; cb += cpr) {
-    const uint32_t c = cb + threadIdx.x / tpc, q = threadIdx.x % tpc;
-    uint32_t cnt = c < c1 ? ld_agent(&a.W.ccnt[c]) : 0u;
-    if (cnt > (uint32_t)kCandSlot) cnt = 0;               // rescanned below
-    for (uint32_t r = q; r < cnt; r += tpc) fn(ld_agent(&a.W.cand[(uint64_t)c * kCandSlot + r]));
-  }
-  for (uint32_t c = c0; c < c1; ++c) {
-    if (ld_agent(&a.W.ccnt[c]) <= (uint32_t)kCandSlot) continue;   // (uniform)
-    const uint32_t base = c * (uint32_t)kChunk;
-    for (uint32_t r = threadIdx.x; r < (uint32_t)kChunk; r += kBlock) {
-      const uint32_t e = base + r;
-      if ((uint64_t)e >= a.n) break;
-      const float x = a.g[e];
-      const uint32_t key = mag_key(x);
-      if (key >= t_lo && key <= t_hi)
-        fn(comp_of(key, e, a.ib) | (uint64_t)(__float_as_uint(x) >> 31) << 63);
-    }
-  }
-}
-
-__device__ __forceinline__ float tail_value(const CompactArgs& a, uint64_t v) {
-  const uint64_t c = v & ~(1ull << 63);
-  const uint32_t key = (uint32_t)(c >> a.ib);
-  if (key >= kNanKey) return a.g[(uint32_t)(c & ((1ull << a.ib) - 1))];   // NaN: its own bits
-  return __uint_as_float(key | (uint32_t)(v >> 63) << 31);
-}
-
-// Resolver ri of R (256 threads).
-__device__ __forceinline__ void dense_tail(const CompactArgs& a, const HdrInit& HI, uint32_t ri,
-                                        uint32_t R, TailShared& ts) {
-  TopkState* S = a.W.st;
-  const int tid = threadIdx.x;
-  uint32_t* h = ts.h;
-  if (tid == 0) {                                         // every chunk group complete
-    uint32_t it = 0;
-    while (ld_agent(&S->tail_top) < R && ++it < kSpinMax) __builtin_amdgcn_s_sleep(2);
-    ts.s_st = it < kSpinMax ? 0u : 1u;
-    ts.s_cnt = 0; ts.s_nmine = 0;
-  }
-  __syncthreads();
-  FC_TR(8);
-  const uint32_t gen0 = ld_agent(&S->gen);               // before the ticket: stable
-  uint32_t se = 0, sc = 0;
-  if (tid < kShards) { se = ld_agent(&S->shard_ent[tid]); sc = ld_agent(&S->shard_cnd[tid]); }
-  const uint32_t t_lo = ld_agent(&S->t_lo), t_hi = ld_agent(&S->t_hi), sbin = ld_agent(&S->sbin);
-  const uint32_t err = ld_agent(&S->err);
-  for (int j = 0; j < kHistBins / kBlock; ++j) h[j * kBlock + tid] = ld_agent(&a.W.chist[j * kBlock + tid]);
-  if (tid < 64) {
-    se = wave_sum(se);
-    sc = wave_sum(sc);
-    if (tid == 0) { ts.s_tot[0] = se; ts.s_tot[1] = sc; }
-  }
-  __syncthreads();
-  const uint64_t k = HI.k;
-  const uint32_t n_ent = ts.s_tot[0], n_cand = ts.s_tot[1], n_hi = n_ent - n_cand;
-  bool retry = ts.s_st != 0 || err || n_cand > n_ent || (uint64_t)n_ent < k || (uint64_t)n_hi > k;
-  const uint32_t rank = retry ? 0u : (uint32_t)(k - n_hi);
-  uint32_t beta = 0, r_in = 1, cnt_beta = 0;
-  if (!retry && rank > 0) {
-    find_rank_desc(h, rank, ts.s_tmp, ts.s_out);
-    beta = ts.s_out[0]; r_in = ts.s_out[1]; cnt_beta = h[beta];
-    retry = cnt_beta > (uint32_t)kSmallCap || cnt_beta < r_in;
-  }
-  __syncthreads();                                        // h is reused (sv) below
-  FC_TR(10);
-  const uint32_t per = (a.nchunks + R - 1) / R;
-  const uint32_t c0 = min(ri * per, a.nchunks), c1 = min(c0 + per, a.nchunks);
-  auto bin_of = [&](uint64_t v) { return ((((uint32_t)((v & ~(1ull << 63)) >> a.ib)) - t_lo) >> sbin); };
-  auto idx_of = [&](uint64_t v) { return (uint32_t)(v & ((1ull << a.ib) - 1)); };
-  if (!retry) {
-    // candidates above beta keep their value, below it go to +0 (rank 0: every one is slack);
-    // bin beta is gathered (LDS, then the workspace list) and kept for after T64
-    tail_cands(a, c0, c1, t_lo, t_hi, [&](uint64_t v) {
-      const uint32_t b = bin_of(v);
-      if (rank > 0 && b > beta) {
-        a.dense[idx_of(v)] = tail_value(a, v);
-      } else if (rank == 0 || b < beta) {
-        a.dense[idx_of(v)] = 0.0f;
-      } else {
-        const uint32_t q = atomicAdd(&ts.s_cnt, 1u);
-        if (q < (uint32_t)kSmallCap) ts.sv[q] = v & ~(1ull << 63);
-        if (q < (uint32_t)kTailMine) ts.mine[q] = v;
-      }
-    });
-    __syncthreads();
-    const uint32_t got = min(ts.s_cnt, (uint32_t)kSmallCap);
-    if (tid == 0 && got) ts.s_base = atomicAdd(&S->small_n, got);
-    __syncthreads();
-    for (uint32_t q = tid; q < got; q += kBlock)
-      if (ts.s_base + q < (uint32_t)kSmallCap) st_agent(&a.W.small[ts.s_base + q], ts.sv[q]);
-  }
-  FC_TR(11);
-  const bool last = last_block_arrive_tree(a.W.tick + kTickWords, R, ri, &ts.s_flag, 16);
-  if (last) {
-    if (tid == 0) st_agent(&S->gen, gen0 + 1u);          // everything is gathered
-  } else if (!retry && rank > 0) {
-    if (tid == 0) {                                       // relaxed sc1 poll (bounded)
-      uint32_t it = 0;
-      while (ld_agent(&S->gen) == gen0 && ++it < kSpinMax) __builtin_amdgcn_s_sleep(4);
-      ts.s_st = it < kSpinMax ? 0u : 1u;
-    }
-    __syncthreads();
-    if (ts.s_st != 0) {                                   // never expected: fail the call
-      if (tid == 0) st_agent(&a.hdr->status, (uint32_t)FC_STATUS_TIMEOUT);
-      return;
-    }
-  }
-  FC_TR(12);
-  // T64 from the gathered list (every resolver picks it itself; rank 0: the definite set)
-  uint64_t T = 0;
-  if (!retry) {
-    if (rank == 0) {
-      T = ((uint64_t)t_hi + 1) << a.ib;
-    } else if (cnt_beta <= (uint32_t)kBlock) {
-      uint64_t m = 0;
-      if ((uint32_t)tid < cnt_beta) { m = ld_agent(&a.W.small[tid]); ts.sv[tid] = m; }
-      __syncthreads();
-      if ((uint32_t)tid < cnt_beta) {
-        uint32_t larger = 0;
-        for (uint32_t j = 0; j < cnt_beta; ++j) larger += ts.sv[j] > m ? 1u : 0u;
-        if (larger == r_in - 1) ts.s_T = m;
-      }
-      __syncthreads();
-      T = ts.s_T;
-    } else {
-      uint32_t P2 = 1;
-      while (P2 < cnt_beta) P2 <<= 1;
-      for (uint32_t i = tid; i < P2; i += kBlock) ts.sv[i] = i < cnt_beta ? ld_agent(&a.W.small[i]) : 0ull;
-      __syncthreads();
-      bitonic_desc(ts.sv, P2, kBlock);
-      T = ts.sv[r_in - 1];
-    }
-    FC_TR(14);
-    if (rank > 0) {                                       // this resolver's bin-beta candidates
-      auto put = [&](uint64_t v) {
-        a.dense[idx_of(v)] = (v & ~(1ull << 63)) >= T ? tail_value(a, v) : 0.0f;
-      };
-      if (ts.s_cnt <= (uint32_t)kTailMine) {
-        for (uint32_t q = tid; q < ts.s_cnt; q += kBlock) put(ts.mine[q]);
-      } else {
-        tail_cands(a, c0, c1, t_lo, t_hi, [&](uint64_t v) { if (bin_of(v) == beta) put(v); });
-      }
-    }
-  }
-  FC_TR(13);
-  if (!last) return;
-  // ---- the last resolver: the header (its only writer in this launch), self-cleaning ----
-  const bool other_err = ld_agent(&S->err) != 0u;
-  for (int b = tid; b < kHistBins; b += kBlock) a.W.chist[b] = 0;
-  if (tid == 0) {
-    fc_packet_hdr* hd = a.hdr;
-    write_hdr_static(hd, HI);
-    hd->lower = ld_agent(&S->L64);
-    hd->thresh = T;
-    hd->n_entries = n_ent;
-    hd->n_definite = n_hi;
-    hd->n_cand = n_cand;
-    if (retry || other_err) hd->status = (uint32_t)FC_STATUS_RETRY_EXACT;
-    S->small_n = 0; S->err = 0; S->tail_top = 0;
-    S->fz_seq += 1u;                                      // the next launch publishes fz_seq + 1
-  }
-  FC_TR(15);
-}
 
 // Candidate binning inside the fused launch (one device-scope atomic per candidate into the
 // candidate histogram) or in k_resolve (rbin) — per variant, see fc_capi.hip
@@ -1231,11 +1000,9 @@ __device__ __forceinline__ void fused_mag_wg(const CompactArgs& a0, const Sample
   __shared__ MagState s_st;
   TopkState* S = a0.W.st;
   const uint32_t pub = sload2(&S->fz_seq).x + 1u;   // not written by this launch
-  constexpr bool kTail = DENSE && FC_DENSE_TAIL != 0 && FC_DENSE_PKT == 0;
   if (blockIdx.x < nsamp) {
     if (threadIdx.x >= kBlock) return;
-    sample_body<kKeyMag, true>(a0.g, P, 0ull, 0ull, a0.W, a0.ib, a0.hdr, HI, blockIdx.x, nsamp, true, u.s,
-                               pub, !kTail);
+    sample_body<kKeyMag, true>(a0.g, P, 0ull, 0ull, a0.W, a0.ib, a0.hdr, HI, blockIdx.x, nsamp, true, u.s, pub);
     return;
   }
   // (chunks in dispatch order: spreading the resident ones over 8 / 64 address streams, as
@@ -1258,28 +1025,7 @@ __device__ __forceinline__ void fused_mag_wg(const CompactArgs& a0, const Sample
   FC_TR(25);
   const MagState st = s_st;
   constexpr bool kBin = DENSE ? FC_FUSED_BIN_DENSE != 0 : FC_FUSED_BIN_PKT != 0;
-  compact_mag_item<NW, MagShared, DENSE, kBin, !DENSE || FC_DENSE_PKT != 0, kTail>(a0, mag_out(a0, 0u), chunk, st, x, u.m);
-  if (kTail) {
-    // completion ticket: every wave drained its slot / count / atomics in the body (its q stores
-    // stay in flight: no vmcnt wait here); the workgroup completing a group resolves
-    __shared__ uint32_t s_role;
-    lds_barrier();
-    if (threadIdx.x == 0) {
-      const uint32_t G = min((uint32_t)kTailGroups, a0.nchunks);
-      const uint32_t gi = chunk % G;
-      const uint32_t gsize = a0.nchunks / G + (gi < a0.nchunks % G ? 1u : 0u);
-      uint32_t role = 0;
-      if (atomicAdd(&a0.W.tgrp[gi * kTickStride], 1u) == gsize - 1) {
-        st_agent(&a0.W.tgrp[gi * kTickStride], 0u);
-        role = 1u + atomicAdd(&S->tail_top, 1u);
-      }
-      s_role = role;
-    }
-    lds_barrier();
-    if (s_role == 0 || threadIdx.x >= kBlock) return;
-    dense_tail(a0, HI, s_role - 1u, min((uint32_t)kTailGroups, a0.nchunks), u.t);
-    return;
-  }
+  compact_mag_item<NW, MagShared, DENSE, kBin, !DENSE || FC_DENSE_PKT != 0>(a0, mag_out(a0, 0u), chunk, st, x, u.m);
 #ifdef FC_ABL_DRAIN
   // ablation (A/B only): what an in-kernel completion count would cost every chunk workgroup —
   // drain its stores (1), plus one atomic on one of 64 group counters (2)
