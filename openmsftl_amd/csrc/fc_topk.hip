@@ -188,9 +188,6 @@ __device__ __forceinline__ void seg_lane(const SamplePlan& P, uint32_t s, int ti
   e = (uint32_t)st + (uint32_t)tid * 4u;
 }
 
-#ifndef FC_PKT_DIRECT
-#define FC_PKT_DIRECT 0       // 1: packet entries straight to the slot, no LDS stage (A/B)
-#endif
 #ifndef FC_SHARDS_ADAPT
 #define FC_SHARDS_ADAPT 1
 #endif
@@ -665,7 +662,7 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
   if (!PKT) {                                           // dense only: q, no entries
 #pragma unroll
     for (int q = 0; q < NQ; ++q) dense_out(q, mag_listed<FAST>(P, x[q]));
-  } else if (!FC_PKT_DIRECT && tot_e <= (uint32_t)SH::kStageN) {   // block-uniform
+  } else if (tot_e <= (uint32_t)SH::kStageN) {          // block-uniform
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const bool p = mag_listed<FAST>(P, x[q]);
@@ -726,7 +723,7 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
     if (tot_c) atomicAdd(&S->shard_cnd[chunk % kShards], tot_c);
   }
   if (!PKT && c_ovf) direct_entries(false);            // rare: the resolve reads them
-  if (PKT && !FC_PKT_DIRECT && tot_e <= (uint32_t)SH::kStageN) {   // coalesced 16-B stores of the staged slot
+  if (PKT && tot_e <= (uint32_t)SH::kStageN) {          // coalesced 16-B stores of the staged slot
     for (uint32_t t = 4 * tid; t < tot_e; t += 4 * MagGeo<NW>::kThreads) {
       if (t + 4 <= tot_e) {
         const uint4 p0 = *reinterpret_cast<const uint4*>(&sh.st[t]);
@@ -1026,16 +1023,6 @@ __device__ __forceinline__ void fused_mag_wg(const CompactArgs& a0, const Sample
   const MagState st = s_st;
   constexpr bool kBin = DENSE ? FC_FUSED_BIN_DENSE != 0 : FC_FUSED_BIN_PKT != 0;
   compact_mag_item<NW, MagShared, DENSE, kBin, !DENSE || FC_DENSE_PKT != 0>(a0, mag_out(a0, 0u), chunk, st, x, u.m);
-#ifdef FC_ABL_DRAIN
-  // ablation (A/B only): what an in-kernel completion count would cost every chunk workgroup —
-  // drain its stores (1), plus one atomic on one of 64 group counters (2)
-  if (DENSE) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (FC_ABL_DRAIN == 2 && threadIdx.x == 0)
-      atomicAdd(reinterpret_cast<uint32_t*>(a0.W.small) + (chunk % 64) * 64, 1u);
-  }
-#endif
   FC_TR(26);
 }
 template <bool DENSE>
