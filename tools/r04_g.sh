@@ -7,6 +7,10 @@ TAG=${1:-r04_g}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread \
+  > $OUT/gpu_tests.log 2>&1 || { tail -40 $OUT/gpu_tests.log; exit 1; }
+tail -1 $OUT/gpu_tests.log
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
 for i in 1 2; do
   timeout -k 10 100 python tools/qsgd_probe.py --n 134217728 --tag qsgd$i >> $OUT/probes.jsonl
 done
