@@ -46,8 +46,9 @@ def parse():
     ap.add_argument("--clients", type=int, default=128, help="clients per GPU")
     ap.add_argument("--n", type=int, default=134_217_728, help="gradient length (fp32)")
     ap.add_argument("--fraction", type=float, default=0.1)
-    ap.add_argument("--streams", type=int, default=2,
-                    help="forked streams the batched encode is split over (1 = one launch chain)")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="forked streams the batched encode is split over (the sub-batches' "
+                         "encodes still run one after the other; 1 = one launch chain)")
     ap.add_argument("--roofline-steps", type=int, default=5,
                     help="extra encode passes with one stream, timed per launch for `roofline`")
     ap.add_argument("--lib", default=None, help="A/B only: load this libfedcodec.so build")
@@ -62,7 +63,7 @@ def parse():
                          "encoded (codec.encode_fold_batch; measured no faster, A/B only)")
     ap.add_argument("--no-batch", action="store_true",
                     help="encode client by client (fc_topk_encode) instead of batched")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r02_pmc_k_compact_mag1.json"),
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r04_pmc_k_compact_mag1.json"),
                     help="PMC summary (profiles/) used for roofline.traffic")
     ap.add_argument("--force-retry-rank", type=int, default=-1,
                     help="test only: on this rank, mark client 0's packet RETRY in the last "
@@ -400,12 +401,12 @@ def main():
     grad_bytes = 4.0 * n * M * world
     value = grad_bytes / (elapsed / args.steps) / 1e9
 
-    # roofline of the dominant kernel (k_compact: the single streaming pass over g).  In the
-    # timed steps two sub-batch launches share the chip (--streams), so a launch's duration is
-    # not its own; the per-launch figure comes from extra passes with ONE launch chain
-    # (per_launch clients per k_compact_mag1 launch, nothing else running), HIP events on the
-    # launch stream.  In a rocprofv3 trace these are the k_compact_mag1 dispatches with
-    # grid.y == per_launch (tools/rocpd_summary.py stats splits dispatches by grid).
+    # roofline of the dominant kernel (k_compact: the single streaming pass over g), HIP events
+    # on the launch stream over the timed steps (one launch chain: per_launch clients per
+    # k_compact_mag1 launch).  With --streams > 1 (sub-batches; a fold may run beside the next
+    # sub-batch's compaction) the per-launch figure comes from extra one-chain passes instead.
+    # In a rocprofv3 trace these are the k_compact_mag1 dispatches with grid.y == per_launch
+    # (tools/rocpd_summary.py stats splits dispatches by grid).
     kt_roof = kt
     if args.roofline_steps > 0 and not args.no_batch and args.streams > 1:
         torch.cuda.synchronize()
@@ -432,9 +433,8 @@ def main():
     breakdown = {c: {"avg_us": round(kt.avg_us(c), 2), "launches": kt.launches[c],
                      "ms_per_step": round(kt.ms[c] / args.steps, 3)}
                  for c in L.TIME_CLASSES if kt.launches.get(c)}
-    breakdown["note"] = ("timed steps; with %d encode streams the compact/sample/engine "
-                         "launches of the sub-batches overlap" % args.streams
-                         if args.streams > 1 and not args.no_batch else "timed steps")
+    breakdown["note"] = ("timed steps; %d sub-batches per step, encoded one after the other"
+                         % args.streams if args.streams > 1 and not args.no_batch else "timed steps")
 
     # whole step against the HBM roofline (SURVEY §8(d) batched FedAvg with fused
     # decode-accumulate: M (4N + 16k) + 4N algorithmic bytes per GPU and step)

@@ -253,6 +253,27 @@ _MAX_SIDE = 4          # GPU_MAX_HW_QUEUES is 4: more forked streams would share
 # batches run on one stream, where at most one client is ever partly dispatched
 # (fc_topk.hip, k_resolve's residency note).  Packets are identical either way.
 _ONE_STREAM_N = 1 << 27
+# Batched encodes on one device never run concurrently: k_sample1 and k_resolve hold a
+# client's workgroups in in-kernel waits, and two such launches on two queues are dispatched
+# to the 8 XCDs interleaved, so each XCD can fill up with waiters whose partners are queued on
+# another full XCD.  Measured on the GPU box: configs[2] with two sub-batches on two streams
+# stalled both k_resolve launches to the spin bound (42 ms, the clients then RETRY) in about 1
+# step in 70.  Each batched launch waits for the device's previous one (an event), whatever
+# stream either is on; one launch alone dispatches its clients in order and always drains.
+_LAST_ENC: dict = {}
+
+
+def _after_last_encode(dev: torch.device, stream) -> None:
+    """Order a batched encode launch on ``stream`` after the device's previous one."""
+    ev = _LAST_ENC.get(dev.index if dev.index is not None else torch.cuda.current_device())
+    if ev is not None:
+        stream.wait_event(ev)
+
+
+def _encode_queued(dev: torch.device, stream) -> None:
+    ev = torch.cuda.Event()
+    ev.record(stream)
+    _LAST_ENC[dev.index if dev.index is not None else torch.cuda.current_device()] = ev
 
 
 def _side_streams(dev: torch.device, count: int = 2) -> list:
@@ -283,13 +304,14 @@ def encode_top_batch(grads: Sequence[torch.Tensor], k: int, *,
                      key_mode: int = L.FC_KEY_MAGNITUDE, seeds=None, offsets=None,
                      packets: Optional[Sequence[Packet]] = None,
                      jobs: Optional[torch.Tensor] = None, check: bool = True,
-                     streams: int = 2, groups: Optional[Sequence[int]] = None,
+                     streams: int = 1, groups: Optional[Sequence[int]] = None,
                      part: int = L.FC_PART_SAMPLE | L.FC_PART_FINISH, fork: bool = True,
                      join: bool = True) -> list:
     """Top-k (or native rand-k) of M equal-length gradients in ONE launch per pipeline stage
     (fc_topk_encode_batch).  Same packets, bit for bit, as M calls of :func:`encode_top`.
     ``jobs``: a prebuilt :func:`encode_jobs` array for these exact grads/packets.
-    ``streams``: sub-batches launched on that many forked streams (joined before return);
+    ``streams``: sub-batches launched on that many forked streams (joined before return), one
+    after the other (batched encodes on a device never overlap: see ``_LAST_ENC``);
     ``groups``: sub-batch sizes (default: ``streams`` equal parts), dealt to the streams in turn.
     Pipelining (bench.py): ``part`` = FC_PART_SAMPLE or FC_PART_FINISH runs one half of the
     pipeline (fc_topk_encode_batch_part; the same ``groups`` / ``streams`` for both halves, so
@@ -352,16 +374,18 @@ def encode_top_batch(grads: Sequence[torch.Tensor], k: int, *,
     if any(x < 1 for x in groups) or sum(groups) != m:
         raise ValueError(f"groups {groups} must be positive sizes summing to {m} clients")
     if nside == 1 or len(groups) == 1:
+        main = torch.cuda.current_stream(dev)
+        _after_last_encode(dev, main)
         ws = BatchWorkspace.get(n, m, dev)
         L.check(lib.fc_topk_encode_batch_part(_vp(jobs), m, n, k, key_mode, packets[0].capacity,
                                               _vp(ws.buf), ws.nbytes, part, _stream(dev)),
                 "fc_topk_encode_batch")
+        _encode_queued(dev, main)
     else:
-        # Sub-batches on forked streams (group i on stream i % streams): one sub-batch's
-        # latency-bound sample/resolve launches run beside another's streaming
-        # k_compact_mag1 (measured 20.6 -> 19.4 ms for 128 clients x 128 M,
-        # tools/overlap_probe.py).  Packets are identical; the caller's stream joins every
-        # fork before this returns, so later work (and frees) stay ordered.
+        # Sub-batches on forked streams (group i on stream i % streams), launched one after
+        # the other (``_LAST_ENC``: two concurrent batched encodes can stall each other to the
+        # spin bound).  Packets are identical; the caller's stream joins every fork before
+        # this returns, so later work (and frees) stay ordered.
         main = torch.cuda.current_stream(dev)
         job_bytes = ctypes.sizeof(L.EncodeJob)
         base = jobs.data_ptr()
@@ -373,12 +397,15 @@ def encode_top_batch(grads: Sequence[torch.Tensor], k: int, *,
                 side.wait_event(ev)
         lo = 0
         for i, size in enumerate(groups):
-            with torch.cuda.stream(sides[i % nside]):
+            side = sides[i % nside]
+            with torch.cuda.stream(side):
+                _after_last_encode(dev, side)
                 ws = BatchWorkspace.get(n, size, dev, slot=i)
                 L.check(lib.fc_topk_encode_batch_part(ctypes.c_void_p(base + lo * job_bytes),
                                                       size, n, k, key_mode, packets[0].capacity,
                                                       _vp(ws.buf), ws.nbytes, part, _stream(dev)),
                         "fc_topk_encode_batch")
+                _encode_queued(dev, side)
             lo += size
         if join:
             for side in sides:
@@ -396,7 +423,8 @@ def encode_fold_batch(grads: Sequence[torch.Tensor], k: int, weights, out: torch
     sub-batch i is encoded on forked stream i and folded there as soon as it is encoded,
     continuing sub-batch i-1's partial sum (an event orders the folds, so the rows are added
     in G's order: bit-identical to :func:`encode_top_batch` + :func:`decode_accumulate`), while
-    sub-batch i+1 still encodes on its own stream.  ``out`` holds the aggregate once the
+    sub-batch i+1 encodes on its own stream (the encodes themselves run one after the other,
+    ``_LAST_ENC``).  ``out`` holds the aggregate once the
     caller's stream (joined at return) reaches it.  Returns an event recorded once every
     sub-batch is ENCODED (the folds may still run); ``status=(src, dst)``: ``dst.copy_(src)``
     (e.g. the packet headers' status words into pinned host memory) is queued right then, so
@@ -433,10 +461,12 @@ def encode_fold_batch(grads: Sequence[torch.Tensor], k: int, weights, out: torch
         side = sides[i]
         with torch.cuda.stream(side):
             side.wait_event(start)
+            _after_last_encode(dev, side)
             ws = BatchWorkspace.get(n, size, dev, slot=i)
             L.check(lib.fc_topk_encode_batch(ctypes.c_void_p(jobs.data_ptr() + lo * jb), size, n, k,
                                              L.FC_KEY_MAGNITUDE, packets[0].capacity, _vp(ws.buf),
                                              ws.nbytes, _stream(dev)), "fc_topk_encode_batch")
+            _encode_queued(dev, side)
             for p, g in zip(packets[lo:hi], grads[lo:hi]):
                 p.k = k
                 p._enc = (g, k, L.FC_KEY_MAGNITUDE, 0, 0)

@@ -1047,13 +1047,15 @@ template __global__ void k_fused_mag<true>(CompactArgs, SamplePlan, HdrInit, uin
 // own range: no fix-up launch (it took 13.8 us per 128 M gradient as its own kernel).
 // The in-kernel waits (beta, "gathered", T64) need every workgroup of a client resident while
 // any of them spins.  A lone encode's grid is <= 512 workgroups (4 per CU by LDS: 1024 slots).
-// A batched launch dispatches its grid in order (x = the client's workgroups, fastest), so at
-// most its LAST client is partly dispatched, and the complete clients before it free the slots
-// it waits for.  Two batched launches on concurrent streams could each hold a partly
-// dispatched client: harmless at <= kResolveGridBatch (16) workgroups per client, so the host
-// side (codec.encode_top_batch) runs batches above 2^27 elements per client, whose clients get
-// up to 512 workgroups (resolve_grid), on ONE stream.  Every spin is bounded (FC_STATUS_TIMEOUT
-// -> the exact path; never expected).
+// A batched launch dispatches its grid in order (x = the client's workgroups, fastest; dealt
+// round-robin to the 8 XCDs, in the same order on each), so at most its LAST client is partly
+// dispatched, and the complete clients before it free the slots it waits for.  Two batched
+// launches on concurrent queues are NOT safe: each XCD interleaves the two grids in its own
+// order, and can fill up with waiters whose partners sit queued behind another full XCD
+// (measured: two 64-client k_resolve launches, 16 workgroups per client, stalled to the spin
+// bound, 42 ms, in ~1 step in 70).  The host side (codec._LAST_ENC) never queues two batched
+// encodes on a device concurrently.  Every spin is bounded (FC_STATUS_TIMEOUT -> the exact
+// path).
 // --------------------------------------------------------------------------------------
 struct ResolveArgs {
   uint32_t ib, nchunks;
