@@ -65,7 +65,11 @@ def main():
                 codec.encode_top_batch(gs, k, packets=pk, jobs=jobs, check=False, streams=1)
             torch.cuda.synchronize()
         codec.resolve(pk)
+        hs = codec.headers(pk)
+        cnt = torch.stack([p.cnt for p in pk]).double()
         res = {c: round(kt.avg_us(c), 2) for c in L.TIME_CLASSES if kt.launches.get(c)}
+        res["entries_over_k"] = round(sum(h.n_entries for h in hs) / (len(hs) * k), 4)
+        res["entries_per_chunk_sd"] = round(float(cnt.std(dim=1).mean()), 1)
         res["compact_GBps_alg"] = round(args.batch * (4.0 * n + 8.0 * k)
                                         / (res["compact"] * 1e-6) / 1e9, 1)
         print(json.dumps({"tag": args.tag, "n": n, "k": k, "batch": args.batch, "avg_us": res}),
