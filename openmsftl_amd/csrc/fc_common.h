@@ -159,6 +159,9 @@ __device__ __forceinline__ float4 load4_plain(const float* __restrict__ g, uint6
   if (e + 3 < n) r.w = g[e + 3];
   return r;
 }
+typedef uint32_t fc_u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t fc_u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t fc_u32x8 __attribute__((ext_vector_type(8)));
 // Unconditional float4 load through the GLOBAL address space.  Pointers that come out of
 // memory (batched job tables) are generic to the compiler, and a generic load is a flat_load
 // that also counts in lgkmcnt; a per-element bounds branch between loads made hipcc wait for

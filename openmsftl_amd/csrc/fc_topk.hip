@@ -583,7 +583,14 @@ struct MagOut {
 // PKT = false (the drop-in dense path, fc_topk_encode_dense): q is the product, the packet
 // entries are not written (-6 B per listed element of HBM writes) except for a chunk whose
 // candidates overflowed their slot (k_resolve re-reads that chunk's entries).
-template <bool FAST, typename SH, int NW, bool DENSE, bool BIN, bool PKT = true>
+// NTS: the packet entries and candidates leave with non-temporal stores.  The batched pass
+// (k_compact_mag1) writes GBs of packets that only the next kernels read back: plain stores left
+// the L2s full of dirty lines that the following k_resolve waited behind (64 x 128 M: compaction
+// 7.24 -> 7.04 ms, resolve 171 -> 140 us; 128 x 16 M: 1.98 -> 1.92 ms, 94 -> 84 us).  A lone
+// encode keeps plain stores: its ~80 MB of entries stay in the Infinity Cache for the decode that
+// usually follows (packet round trip at 128 M: 260 us plain, 294 us non-temporal;
+// profiles/r04_ab_entry_nt_stores.jsonl).
+template <bool FAST, typename SH, int NW, bool DENSE, bool BIN, bool PKT = true, bool NTS = false>
 __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred& P,
                                                  float (&x)[MagGeo<NW>::kQ], SH& sh,
                                                  uint32_t chunk, uint32_t sbin) {
@@ -728,9 +735,19 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
       if (t + 4 <= tot_e) {
         const uint4 p0 = *reinterpret_cast<const uint4*>(&sh.st[t]);
         const uint4 p1 = *reinterpret_cast<const uint4*>(&sh.st[t + 2]);
-        *reinterpret_cast<uint2*>(a.idx + slot + t) =      // 4 chunk-local u16 indices
-            make_uint2(p0.x | (p0.z << 16), p1.x | (p1.z << 16));
-        *reinterpret_cast<uint4*>(a.val + slot + t) = make_uint4(p0.y, p0.w, p1.y, p1.w);
+        fc_u32x2 iv;                                       // 4 chunk-local u16 indices
+        iv.x = p0.x | (p0.z << 16); iv.y = p1.x | (p1.z << 16);
+        fc_u32x4 vv;
+        vv.x = p0.y; vv.y = p0.w; vv.z = p1.y; vv.w = p1.w;
+        fc_u32x2* ip = reinterpret_cast<fc_u32x2*>(a.idx + slot + t);
+        fc_u32x4* vp = reinterpret_cast<fc_u32x4*>(a.val + slot + t);
+        if (NTS) {
+          __builtin_nontemporal_store(iv, ip);
+          __builtin_nontemporal_store(vv, vp);
+        } else {
+          *ip = iv;
+          *vp = vv;
+        }
       } else {
         for (uint32_t u = t; u < tot_e; ++u) {
           a.idx[slot + u] = (uint16_t)sh.st[u].x;
@@ -752,7 +769,11 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
     }
     if (p < nj) {
       if (BIN) atomicAdd(&a.chist[sh.cstb[tid]], 1u);
-      if (!c_ovf) a.cand[(uint64_t)chunk * kCandSlot + pre + p] = sh.cst[tid];
+      if (!c_ovf) {
+        uint64_t* cp = &a.cand[(uint64_t)chunk * kCandSlot + pre + p];
+        if (NTS) __builtin_nontemporal_store(sh.cst[tid], cp);
+        else *cp = sh.cst[tid];
+      }
     }
   }
 }
@@ -761,9 +782,6 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
 // launch writes them, but they sit behind generic pointers, so hipcc issued vector loads and
 // waited for them (vmcnt(0)) in front of the gradient loads: one extra serialized HBM/L2
 // latency per workgroup.  Reading through the scalar cache is fine (nothing here writes it).
-typedef uint32_t fc_u32x2 __attribute__((ext_vector_type(2)));
-typedef uint32_t fc_u32x4 __attribute__((ext_vector_type(4)));
-typedef uint32_t fc_u32x8 __attribute__((ext_vector_type(8)));
 __device__ __forceinline__ fc_u32x2 sload2(const void* p) {
   fc_u32x2 v;
   asm volatile("s_load_dwordx2 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
@@ -863,7 +881,7 @@ __device__ __forceinline__ void mag_load(const float* g, uint32_t chunk, uint64_
 // workgroups per CU overlap one another's load latency.  (A persistent variant that kept the
 // next item's loads in flight measured 1.3-2.5x SLOWER: hipcc spilled the second register set
 // and loop-carried state)
-template <int NW, typename SH, bool DENSE, bool BIN, bool PKT = true>
+template <int NW, typename SH, bool DENSE, bool BIN, bool PKT = true, bool NTS = false>
 __device__ __forceinline__ void compact_mag_item(const CompactArgs& a0, const MagOut& o,
                                                  uint32_t chunk, const MagState& st,
                                                  float (&x)[MagGeo<NW>::kQ], SH& sh) {
@@ -885,7 +903,7 @@ __device__ __forceinline__ void compact_mag_item(const CompactArgs& a0, const Ma
   P.cand_all = P.t_hi >= 0x7f800001u;
   P.T_hi = __uint_as_float(P.cand_all ? 0x7f800000u : P.t_hi);
   if (fast) {
-    compact_mag_body<true, SH, NW, DENSE, BIN, PKT>(o, P, x, sh, chunk, st.sbin);
+    compact_mag_body<true, SH, NW, DENSE, BIN, PKT, NTS>(o, P, x, sh, chunk, st.sbin);
   } else if (none) {                                       // k = 0: nothing listed
     SH::barrier();
     if (tid == 0) {
@@ -898,7 +916,7 @@ __device__ __forceinline__ void compact_mag_item(const CompactArgs& a0, const Ma
         o.dense[base + i] = 0.0f;
   } else {                                                 // rare: exact integer predicate
     mag_exact_bits<NW>(P, x, base + (uint32_t)((tid >> 6) * 256 + lane_id()));
-    compact_mag_body<false, SH, NW, DENSE, BIN, PKT>(o, P, x, sh, chunk, st.sbin);
+    compact_mag_body<false, SH, NW, DENSE, BIN, PKT, NTS>(o, P, x, sh, chunk, st.sbin);
   }
 }
 
@@ -938,7 +956,7 @@ __device__ __forceinline__ void mag_item_of(uint32_t& client, uint32_t& chunk) {
 #endif
 }
 
-template <int NW, bool DENSE = false>
+template <int NW, bool DENSE = false, bool NTS = false>
 __device__ __forceinline__ void compact_mag_wg(const CompactArgs& a0) {
   __shared__ __attribute__((aligned(16))) MagShared sh;
   uint32_t client, chunk;
@@ -946,11 +964,11 @@ __device__ __forceinline__ void compact_mag_wg(const CompactArgs& a0) {
   float x[MagGeo<NW>::kQ];
   mag_load<NW>(mag_g(a0, client), chunk, a0.n, x);       // g first, state behind it
   const MagState st = mag_state(mag_S(a0, client));
-  compact_mag_item<NW, MagShared, DENSE, false>(a0, mag_out(a0, client), chunk, st, x, sh);
+  compact_mag_item<NW, MagShared, DENSE, false, true, NTS>(a0, mag_out(a0, client), chunk, st, x, sh);
 }
 // 512 threads (8 waves x 16 elements per lane)
 __global__ __launch_bounds__(kCBlock, FC_MAG1_WAVES_PER_EU) void k_compact_mag1(CompactArgs a0) {
-  compact_mag_wg<8>(a0);
+  compact_mag_wg<8, false, true>(a0);
 }
 // the same pass that also streams the dense result q (fc_topk_encode_dense; one client)
 __global__ __launch_bounds__(kCBlock, FC_MAG1_WAVES_PER_EU) void k_compact_mag1_dense(CompactArgs a0) {
