@@ -461,6 +461,40 @@ def test_batch_encode_forked_streams(streams, groups):
         _check_top_packet(x, k, pb, codec.decode(pb).cpu().numpy())
 
 
+@pytest.mark.timeout(120)
+def test_batch_encodes_on_forked_streams_never_overlap():
+    """Two batched encodes must not run concurrently on one device: k_resolve's in-kernel waits
+    can then stall to the spin bound and the clients come back RETRY.  Without the per-device
+    ordering (codec._LAST_ENC) this loop — 2 x 64 clients of 4 M on two streams, steps queued
+    back to back with a FedAVG fold between them — hit it in 23 of 1,500 steps
+    (tools/stall_probe.py --off); with it, every status of 600 steps stays OK (counted on the
+    device after each step, no host sync)."""
+    codec = _codec()
+    from openmsftl_amd import _lib as L
+    n, M, f = 1 << 22, 128, 0.1
+    dev = torch.device("cuda", 0)
+    gen = torch.Generator(device="cuda").manual_seed(9)
+    grads = [torch.randn(n, device="cuda", generator=gen) * (10.0 ** (-4 + 3 * (i % 7) / 6))
+             for i in range(M)]
+    k = co.effective_k(co.num_kept(f, n), n)
+    hdrs = torch.zeros((M, L.HDR_BYTES), dtype=torch.uint8, device=dev)
+    pk = [codec.Packet.alloc(n, L.FC_FMT_IDXVAL, dev, hdr=hdrs[j], k=k) for j in range(M)]
+    codec.encode_top_batch(grads, k, packets=pk)
+    jobs = codec.encode_jobs(grads, pk)
+    w = [1.0 / M] * M
+    views = codec.views_tensor(pk, w, dev)
+    acc = torch.empty(n, dtype=torch.float32, device=dev)
+    bad = torch.zeros((), dtype=torch.int64, device=dev)
+    status = hdrs[:, 36:40]
+    for _ in range(600):
+        codec.encode_top_batch(grads, k, packets=pk, jobs=jobs, check=False, streams=2)
+        bad += (status != 0).any(dim=1).sum()
+        codec.decode_accumulate(pk, w, out=acc, views=views)
+    torch.cuda.synchronize()
+    assert int(bad) == 0, f"{int(bad)} client statuses not OK (stalled k_resolve -> RETRY)"
+    assert codec.resolve(pk) == 0
+
+
 @pytest.mark.parametrize("M,streams", [(5, 2), (7, 3), (2, 2), (1, 2)])
 def test_encode_fold_batch_pipelined(M, streams):
     """encode_fold_batch (each sub-batch folded on its stream as soon as it is encoded, the
