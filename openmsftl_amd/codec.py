@@ -13,7 +13,9 @@ Plus per-chunk counts and quarter offsets and a 96-byte device header (``fc_pack
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
+import threading
 import weakref
 from dataclasses import dataclass
 from typing import Optional, Sequence
@@ -175,9 +177,10 @@ def encode_top(g: torch.Tensor, k: int, *, key_mode: int = L.FC_KEY_MAGNITUDE, s
         packet = Packet.alloc(n, L.FC_FMT_IDXVAL, g.device, k=k)
     packet.k = k
     fn = lib.fc_topk_encode_exact if exact else lib.fc_topk_encode
-    L.check(fn(_vp(g), n, k, key_mode, seed, offset, _vp(packet.idx), _vp(packet.val),
-               packet.capacity, _vp(packet.cnt), _vp(packet.qoff), _vp(packet.hdr), _vp(ws.buf),
-               ws.nbytes, _stream(g.device)), "fc_topk_encode")
+    with _ordered_encode(g.device):
+        L.check(fn(_vp(g), n, k, key_mode, seed, offset, _vp(packet.idx), _vp(packet.val),
+                   packet.capacity, _vp(packet.cnt), _vp(packet.qoff), _vp(packet.hdr), _vp(ws.buf),
+                   ws.nbytes, _stream(g.device)), "fc_topk_encode")
     packet._enc = (g, k, key_mode, seed, offset)
     packet._dense_only = False
     if check:
@@ -208,10 +211,11 @@ def compress_top_dense(g: torch.Tensor, k: int, out: Optional[torch.Tensor] = No
     lib = L.load()
     ws = Workspace.get(n, g.device)
     packet.k = k
-    L.check(lib.fc_topk_encode_dense(_vp(g), n, k, _vp(packet.idx), _vp(packet.val),
-                                     packet.capacity, _vp(packet.cnt), _vp(packet.qoff),
-                                     _vp(packet.hdr), _vp(ws.buf), ws.nbytes, _vp(out),
-                                     _stream(g.device)), "fc_topk_encode_dense")
+    with _ordered_encode(g.device):
+        L.check(lib.fc_topk_encode_dense(_vp(g), n, k, _vp(packet.idx), _vp(packet.val),
+                                         packet.capacity, _vp(packet.cnt), _vp(packet.qoff),
+                                         _vp(packet.hdr), _vp(ws.buf), ws.nbytes, _vp(out),
+                                         _stream(g.device)), "fc_topk_encode_dense")
     packet._enc = (g, k, L.FC_KEY_MAGNITUDE, 0, 0)
     packet._dense_only = True
     if check and resolve([packet]):            # bracket missed: exact packet, then decode
@@ -253,27 +257,34 @@ _MAX_SIDE = 4          # GPU_MAX_HW_QUEUES is 4: more forked streams would share
 # batches run on one stream, where at most one client is ever partly dispatched
 # (fc_topk.hip, k_resolve's residency note).  Packets are identical either way.
 _ONE_STREAM_N = 1 << 27
-# Batched encodes on one device never run concurrently: k_sample1 and k_resolve hold a
-# client's workgroups in in-kernel waits, and two such launches on two queues are dispatched
-# to the 8 XCDs interleaved, so each XCD can fill up with waiters whose partners are queued on
+# Encodes on one device never run concurrently.  k_fused_mag, k_sample1 and k_resolve hold a
+# client's workgroups in in-kernel waits, and two such launches on two queues are dispatched to
+# the 8 XCDs interleaved, so each XCD can fill up with waiters whose partners are queued on
 # another full XCD.  Measured on the GPU box: configs[2] with two sub-batches on two streams
 # stalled both k_resolve launches to the spin bound (42 ms, the clients then RETRY) in about 1
-# step in 70.  Each batched launch waits for the device's previous one (an event), whatever
-# stream either is on; one launch alone dispatches its clients in order and always drains.
-_LAST_ENC: dict = {}
+# step in 70 (tools/stall_probe.py).  Lone encodes of one length also share one Workspace.
+# Every encode launch is therefore ordered after the device's previous one: when it is queued
+# on another stream than that one, it waits for an event recorded there (nothing is recorded
+# while the encodes stay on one stream).  One launch alone dispatches its clients in order and
+# always drains.
+_LAST_ENC: dict = {}                    # device index -> stream of the last encode queued there
+_ENC_LOCK = threading.RLock()
 
 
-def _after_last_encode(dev: torch.device, stream) -> None:
-    """Order a batched encode launch on ``stream`` after the device's previous one."""
-    ev = _LAST_ENC.get(dev.index if dev.index is not None else torch.cuda.current_device())
-    if ev is not None:
-        stream.wait_event(ev)
-
-
-def _encode_queued(dev: torch.device, stream) -> None:
-    ev = torch.cuda.Event()
-    ev.record(stream)
-    _LAST_ENC[dev.index if dev.index is not None else torch.cuda.current_device()] = ev
+@contextlib.contextmanager
+def _ordered_encode(dev: torch.device):
+    """Queue the encode launched inside this block on the current stream after the device's
+    previous encode (held under a lock, so another host thread cannot slip in between)."""
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    stream = torch.cuda.current_stream(dev)
+    with _ENC_LOCK:
+        last = _LAST_ENC.get(key)
+        if last is not None and last != stream:
+            ev = torch.cuda.Event()
+            ev.record(last)
+            stream.wait_event(ev)
+        yield
+        _LAST_ENC[key] = stream
 
 
 def _side_streams(dev: torch.device, count: int = 2) -> list:
@@ -374,13 +385,11 @@ def encode_top_batch(grads: Sequence[torch.Tensor], k: int, *,
     if any(x < 1 for x in groups) or sum(groups) != m:
         raise ValueError(f"groups {groups} must be positive sizes summing to {m} clients")
     if nside == 1 or len(groups) == 1:
-        main = torch.cuda.current_stream(dev)
-        _after_last_encode(dev, main)
         ws = BatchWorkspace.get(n, m, dev)
-        L.check(lib.fc_topk_encode_batch_part(_vp(jobs), m, n, k, key_mode, packets[0].capacity,
-                                              _vp(ws.buf), ws.nbytes, part, _stream(dev)),
-                "fc_topk_encode_batch")
-        _encode_queued(dev, main)
+        with _ordered_encode(dev):
+            L.check(lib.fc_topk_encode_batch_part(_vp(jobs), m, n, k, key_mode, packets[0].capacity,
+                                                  _vp(ws.buf), ws.nbytes, part, _stream(dev)),
+                    "fc_topk_encode_batch")
     else:
         # Sub-batches on forked streams (group i on stream i % streams), launched one after
         # the other (``_LAST_ENC``: two concurrent batched encodes can stall each other to the
@@ -398,14 +407,12 @@ def encode_top_batch(grads: Sequence[torch.Tensor], k: int, *,
         lo = 0
         for i, size in enumerate(groups):
             side = sides[i % nside]
-            with torch.cuda.stream(side):
-                _after_last_encode(dev, side)
+            with torch.cuda.stream(side), _ordered_encode(dev):
                 ws = BatchWorkspace.get(n, size, dev, slot=i)
                 L.check(lib.fc_topk_encode_batch_part(ctypes.c_void_p(base + lo * job_bytes),
                                                       size, n, k, key_mode, packets[0].capacity,
                                                       _vp(ws.buf), ws.nbytes, part, _stream(dev)),
                         "fc_topk_encode_batch")
-                _encode_queued(dev, side)
             lo += size
         if join:
             for side in sides:
@@ -461,12 +468,12 @@ def encode_fold_batch(grads: Sequence[torch.Tensor], k: int, weights, out: torch
         side = sides[i]
         with torch.cuda.stream(side):
             side.wait_event(start)
-            _after_last_encode(dev, side)
             ws = BatchWorkspace.get(n, size, dev, slot=i)
-            L.check(lib.fc_topk_encode_batch(ctypes.c_void_p(jobs.data_ptr() + lo * jb), size, n, k,
-                                             L.FC_KEY_MAGNITUDE, packets[0].capacity, _vp(ws.buf),
-                                             ws.nbytes, _stream(dev)), "fc_topk_encode_batch")
-            _encode_queued(dev, side)
+            with _ordered_encode(dev):
+                L.check(lib.fc_topk_encode_batch(ctypes.c_void_p(jobs.data_ptr() + lo * jb), size, n,
+                                                 k, L.FC_KEY_MAGNITUDE, packets[0].capacity,
+                                                 _vp(ws.buf), ws.nbytes, _stream(dev)),
+                        "fc_topk_encode_batch")
             for p, g in zip(packets[lo:hi], grads[lo:hi]):
                 p.k = k
                 p._enc = (g, k, L.FC_KEY_MAGNITUDE, 0, 0)
@@ -506,10 +513,11 @@ def resolve(packets: Sequence[Packet]) -> int:
             raise L.FedCodecError(f"packet status {h.status}")
         g, k, key_mode, seed, offset = p._enc
         ws = Workspace.get(g.numel(), g.device)
-        L.check(lib.fc_topk_encode_exact(_vp(g), g.numel(), k, key_mode, seed, offset,
-                                         _vp(p.idx), _vp(p.val), p.capacity, _vp(p.cnt),
-                                         _vp(p.qoff), _vp(p.hdr), _vp(ws.buf), ws.nbytes,
-                                         _stream(g.device)), "fc_topk_encode_exact")
+        with _ordered_encode(g.device):
+            L.check(lib.fc_topk_encode_exact(_vp(g), g.numel(), k, key_mode, seed, offset,
+                                             _vp(p.idx), _vp(p.val), p.capacity, _vp(p.cnt),
+                                             _vp(p.qoff), _vp(p.hdr), _vp(ws.buf), ws.nbytes,
+                                             _stream(g.device)), "fc_topk_encode_exact")
         redo += 1
         p._dense_only = False                        # a full packet now
         h2 = p.header()
@@ -533,11 +541,12 @@ def encode_mask(g: torch.Tensor, codec: int, *, p: float = 0.5,
         raise ValueError("mask_bits must be an int32 CUDA tensor of ceil(n/32) words")
     if packet is None:
         packet = Packet.alloc(n, fmt, g.device)
-    L.check(lib.fc_mask_encode(_vp(g), n, codec, _vp(mask_bits), float(p), seed, offset, fmt,
-                               _vp(packet.idx), _vp(packet.val), _vp(packet.bitmap),
-                               packet.capacity, _vp(packet.cnt), _vp(packet.qoff),
-                               _vp(packet.hdr), _vp(ws.buf), ws.nbytes, _stream(g.device)),
-            "fc_mask_encode")
+    with _ordered_encode(g.device):
+        L.check(lib.fc_mask_encode(_vp(g), n, codec, _vp(mask_bits), float(p), seed, offset, fmt,
+                                   _vp(packet.idx), _vp(packet.val), _vp(packet.bitmap),
+                                   packet.capacity, _vp(packet.cnt), _vp(packet.qoff),
+                                   _vp(packet.hdr), _vp(ws.buf), ws.nbytes, _stream(g.device)),
+                "fc_mask_encode")
     return packet
 
 
@@ -685,15 +694,17 @@ def compress_top_dense_f64(g: torch.Tensor, k: int, *, key_mode: int = L.FC_KEY_
                and g.data_ptr() % 16 == 0 and out.data_ptr() % 16 == 0)
     if sampled:
         st = _f64_status(g.device)
-        L.check(lib.fc_topk_dense_f64_sampled(_vp(g), n, k, _vp(out), _vp(ws.buf), ws.nbytes,
-                                              _vp(st), _stream(g.device)),
-                "fc_topk_dense_f64_sampled")
+        with _ordered_encode(g.device):
+            L.check(lib.fc_topk_dense_f64_sampled(_vp(g), n, k, _vp(out), _vp(ws.buf), ws.nbytes,
+                                                  _vp(st), _stream(g.device)),
+                    "fc_topk_dense_f64_sampled")
         out._fc_f64_enc = (g, k)
         if check:
             resolve_f64(out)
         return out
-    L.check(lib.fc_topk_dense_f64(_vp(g), n, k, key_mode, seed, offset, _vp(out), _vp(ws.buf),
-                                  ws.nbytes, _stream(g.device)), "fc_topk_dense_f64")
+    with _ordered_encode(g.device):
+        L.check(lib.fc_topk_dense_f64(_vp(g), n, k, key_mode, seed, offset, _vp(out), _vp(ws.buf),
+                                      ws.nbytes, _stream(g.device)), "fc_topk_dense_f64")
     return out
 
 
