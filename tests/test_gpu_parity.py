@@ -403,7 +403,10 @@ def test_batch_encode_above_resolve_chunk_list():
              .mul_(10.0 ** -s) for s in range(M)]
     k = co.num_kept(0.1, n)
     from openmsftl_amd import _lib as L
-    pk = codec.encode_top_batch(grads, k, check=False)
+    pk = codec.encode_top_batch(grads, k, check=False, streams=2)   # (> 2^27 and
+    torch.cuda.synchronize()                                         # two streams: no timeouts)
+    assert [int(h.status) for h in codec.headers(pk)] == [0] * M
+    pk = codec.encode_top_batch(grads, k, packets=pk, check=False)
     torch.cuda.synchronize()
     assert [int(h.status) for h in codec.headers(pk)] == [0] * M
     for g, pb in zip(grads, pk):
