@@ -24,6 +24,14 @@
  * workspace); return 0 on success, <0 on argument / HIP errors (fc_last_error() explains,
  * thread-local).  Device-side outcomes (e.g. the sampled bracket missing) are reported in the
  * packet header's `status`, read by the host after the stream is synchronised.
+ *
+ * One encode at a time per device: the encode kernels (fc_topk_encode*, fc_topk_encode_batch*,
+ * fc_mask_encode, fc_topk_dense_f64*) hold a client's workgroups in bounded in-kernel waits that
+ * assume no OTHER such kernel is dispatched beside them; two of them on two streams of one
+ * device can stall each other to the bound (the clients then report FC_STATUS_TIMEOUT /
+ * FC_STATUS_RETRY_EXACT: correct after the exact re-encode, but ~40 ms late).  Queue encodes on
+ * one stream, or order them with events (the Python layer does: codec._ordered_encode).
+ * Decodes, folds and sums have no such waits and may run beside anything.
  */
 #ifndef FEDCODEC_H_
 #define FEDCODEC_H_
