@@ -143,10 +143,23 @@ def cpu_baseline(n, fraction):
     q, dt = _timed(lambda: co.compress(cfg, g, argsort_kind=None))
     assert q.shape == g.shape
     return {"value": round(4.0 * n / dt / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
+            "cpu_model": _cpu_model(),
             "sample": f"1 client x {n:,} fp32, top f={fraction}: the reference's exact NumPy "
                       f"calls (compression.py:31-37, default-kind argsort; "
                       f"oracle/compression_oracle.py argsort_kind=None), single-threaded; "
                       f"{dt:.2f} s on {os.cpu_count()} visible host cores (1 used)"}
+
+
+def _cpu_model() -> str:
+    """The host CPU's model name (record it beside the CPU baseline)."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def cpu_matrix(n16=16_777_216, n25=25_557_032):
