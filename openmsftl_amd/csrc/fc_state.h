@@ -36,11 +36,17 @@ struct alignas(16) TopkState {
 };
 static_assert(sizeof(TopkState) <= 1024, "state block");
 
+// Histogram shards (the sample's and the resolve's candidate histogram): fewer shards queue more
+// same-address flush atomics but give the last arriver fewer loads, and its loads are on the
+// latency chain.  Measured (profiles/r04_ab_hist_shards.jsonl): lone 16 M dense encode 57.5 ->
+// 52 us with ONE sample shard for its 128 sample workgroups, 128 M best at two; the batched
+// resolve 84 -> 78 us and the lone packet resolve 24 -> 23 us with two candidate shards (one:
+// 26 us); eight candidate shards +50 %.
 #ifndef FC_SAMPLE_SHARDS
-#define FC_SAMPLE_SHARDS 8
+#define FC_SAMPLE_SHARDS 2
 #endif
 #ifndef FC_CAND_SHARDS
-#define FC_CAND_SHARDS 4
+#define FC_CAND_SHARDS 2
 #endif
 constexpr int kSampleShards = FC_SAMPLE_SHARDS;   // k_sample1's global histogram, sharded by workgroup
 constexpr int kCandShards = FC_CAND_SHARDS;       // k_resolve's candidate histogram, likewise

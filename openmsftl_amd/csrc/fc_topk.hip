@@ -188,9 +188,6 @@ __device__ __forceinline__ void seg_lane(const SamplePlan& P, uint32_t s, int ti
   e = (uint32_t)st + (uint32_t)tid * 4u;
 }
 
-#ifndef FC_SHARDS_ADAPT
-#define FC_SHARDS_ADAPT 1
-#endif
 // gh[b] += h[b] for the non-empty bins of a 4096-bin LDS histogram (256 threads).  (Two bins
 // per 64-bit atomic measured SLOWER: +10 us per lone encode, the last arriver's shard loads
 // queued behind the 64-bit atomics, profiles/r04_ab_sample_chain.jsonl.)
@@ -361,9 +358,9 @@ __device__ __forceinline__ void sample_body(const T* __restrict__ g, const Sampl
   }
   __syncthreads();
   FC_TR(3);
-  // histogram shards: one per 32 workgroups (<= kSampleShards): a small launch's last arriver
-  // then sums fewer shards (a lone 16 M encode has 128 sample workgroups)
-  const uint32_t nsh = FC_SHARDS_ADAPT ? min((uint32_t)kSampleShards, max(1u, nb / 32u)) : (uint32_t)kSampleShards;
+  // histogram shards: one per 128 workgroups (<= kSampleShards): the last arriver's shard loads
+  // are on the bracket's latency chain (a lone 16 M encode has 128 sample workgroups: one shard)
+  const uint32_t nsh = min((uint32_t)kSampleShards, max(1u, nb / 128u));
   flush_hist(W.hist1 + (bid % nsh) * kHistBins, h);   // into this workgroup's shard
   FC_TR(4);
   if (!last_block_arrive_tree(W.tick, nb, bid, &sm.s_flag, 18)) return;
@@ -1210,9 +1207,9 @@ __global__ __launch_bounds__(kBlock) void k_resolve(ResolveArgs a0) {
     }
   };
   // ---- the candidate histogram: every workgroup bins the candidates of its chunk range in
-  // LDS and flushes the non-empty bins into one of kCandShards (4) shards (one shared
-  // histogram queued ~94 same-address atomics per bin with 256 workgroups; 8 or 16 shards
-  // measured no better for a batch's 16 per client); the last arriver (two-level ticket)
+  // LDS and flushes the non-empty bins into one of kCandShards (2) shards (one shared
+  // histogram: its queued same-address atomics cost the lone encode 3 us; 4 / 8 shards: the
+  // last arriver's extra shard loads cost more, fc_state.h); the last arriver (two-level ticket)
   // sums the shards, finds the bin beta holding rank r and publishes it (generation word
   // hgen).  (The compaction used to add every candidate into the histogram with a global
   // atomic: 5.7 % of that pass at 128 M.)  The wait
