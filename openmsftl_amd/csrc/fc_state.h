@@ -65,6 +65,12 @@ struct WsLayout {
     L.off_hist1 = o;  o += 4ull * kHistBins * kSampleShards;
     L.off_tick = o;   o += 4ull * kTickWords * 3;      // sample, resolve (gather), resolve (bins)
     L.off_ehist = o;  o += 4ull * kHistBins;
+    // 8 KB of padding before the candidate histogram, which the drop-in dense encode hits with
+    // one device atomic per candidate while it streams: at offset 63,232 (no padding) the lone
+    // 16 M dense encode took 55.6 us and 128 M 219 us, with 4 / 8 / 16 KB of padding 51 us and
+    // 211-214 us (2 KB: no change) — an HBM channel / bank collision of those atomics with
+    // another hot line of the launch (profiles/r04_ab_chist_offset.jsonl)
+    o += 8192;
     L.off_chist = o;  o += 4ull * kHistBins * kCandShards;
     L.off_small = o;  o += 8ull * kSmallCap;
     L.off_status = o; o += 4ull * (L.nchunks ? L.nchunks : 1);   // per-chunk candidate counts
