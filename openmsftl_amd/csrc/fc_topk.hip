@@ -995,12 +995,16 @@ union FusedShared {
 };
 
 // Candidate binning inside the fused launch (one device-scope atomic per candidate into the
-// candidate histogram) or in k_resolve (rbin) — per variant, see fc_capi.hip
+// candidate histogram) or in k_resolve (rbin) — per variant, see fc_capi.hip.  Both lone paths
+// bin in-kernel since round 4: with the candidate histogram at its padded workspace offset
+// (fc_state.h) the atomics cost the 128 M packet encode +2 us in the fused kernel and save 8 us
+// of resolve (170 -> 165 us; 16 M: equal).  Round 3 had measured 197 vs 148 us — the
+// histogram's lines then collided in HBM with another hot line (profiles/r04_ab_fused_bin.jsonl).
 #ifndef FC_FUSED_BIN_DENSE
 #define FC_FUSED_BIN_DENSE 1
 #endif
 #ifndef FC_FUSED_BIN_PKT
-#define FC_FUSED_BIN_PKT 0
+#define FC_FUSED_BIN_PKT 1
 #endif
 #ifndef FC_DENSE_PKT
 #define FC_DENSE_PKT 0        // 1: the dense path also writes every packet entry (A/B only)
