@@ -236,6 +236,11 @@ int fc_decode_accumulate_continue(const fc_packet_view* views_dev, int m, int fo
  * pointers, w = DEVICE fp32[m]. */
 int fc_weighted_sum_dense(const float* const* rows, const float* w, int m, uint64_t n,
                           float* out, fc_stream_t stream);
+/* Same sum continuing the partial sum already in out (out = fl(out + fl(w_i * row_i)) for
+ * i = 0..m-1): 'full' rows streamed group by group from host memory (aggregation.py:61-63)
+ * fold to the same bits as one call over all rows. */
+int fc_weighted_sum_dense_continue(const float* const* rows, const float* w, int m, uint64_t n,
+                                   float* out, fc_stream_t stream);
 
 /* ---- flat-layout staging on the device (model_helper.py:11-35, client.py:44,52-53) ------
  * params_dev: DEVICE array of `count` fp32 parameter pointers; offsets_dev: DEVICE

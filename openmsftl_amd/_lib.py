@@ -88,6 +88,7 @@ SIGNATURES = {
     "fc_decode_accumulate": (_i32, [_vp, _i32, _i32, _u64, _vp, _vp]),
     "fc_decode_accumulate_continue": (_i32, [_vp, _i32, _i32, _u64, _vp, _vp]),
     "fc_weighted_sum_dense": (_i32, [_vp, _vp, _i32, _u64, _vp, _vp]),
+    "fc_weighted_sum_dense_continue": (_i32, [_vp, _vp, _i32, _u64, _vp, _vp]),
     "fc_div_scalar": (_i32, [_vp, _u64, ctypes.c_float, _vp]),
     "fc_flat_stage": (_i32, [_vp, _vp, _i32, _u64, _vp, _vp, _i32, _vp]),
     "fc_qsgd_code_words": (_u64, [_u64, _i32]),

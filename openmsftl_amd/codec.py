@@ -607,7 +607,8 @@ def weighted_sum_dense(rows, weights: torch.Tensor, out: Optional[torch.Tensor] 
 
     float32 rows and float32 weights: fp32 arithmetic (k_wsum).  Anything float64 (rows,
     weights or ``out_dtype``): NumPy's promotion of ``G * w`` to float64, fp64 arithmetic
-    (k_wsum64); the result is float64."""
+    (k_wsum64); the result is float64.  ``continue_sum``: ``out`` holds the sum of earlier
+    rows and these rows continue it (same bits as one call over all rows)."""
     lib = L.load()
     if isinstance(rows, torch.Tensor):
         rows = list(rows.unbind(0))
@@ -634,11 +635,9 @@ def weighted_sum_dense(rows, weights: torch.Tensor, out: Optional[torch.Tensor] 
                                               len(rows), n, _vp(out), int(continue_sum),
                                               _stream(dev)), "fc_weighted_sum_dense_f64")
         return out
-    if continue_sum:
-        raise ValueError("continue_sum is a float64-path option")
     w = weights.to(device=dev, dtype=torch.float32).contiguous()
-    L.check(lib.fc_weighted_sum_dense(_vp(ptrs), _vp(w), len(rows), n, _vp(out), _stream(dev)),
-            "fc_weighted_sum_dense")
+    fn = lib.fc_weighted_sum_dense_continue if continue_sum else lib.fc_weighted_sum_dense
+    L.check(fn(_vp(ptrs), _vp(w), len(rows), n, _vp(out), _stream(dev)), "fc_weighted_sum_dense")
     return out
 
 

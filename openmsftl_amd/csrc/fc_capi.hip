@@ -774,8 +774,8 @@ int fc_div_scalar(float* x, uint64_t n, float d, fc_stream_t stream) {
   return FC_OK;
 }
 
-int fc_weighted_sum_dense(const float* const* rows, const float* w, int m, uint64_t n,
-                          float* out, fc_stream_t stream) {
+static int weighted_sum_dense(const float* const* rows, const float* w, int m, uint64_t n,
+                              float* out, int acc_in, fc_stream_t stream) {
   FC_CHECK(rows && w && out, "NULL argument");
   FC_CHECK(m >= 1, "m=%d < 1", m);
   FC_CHECK(n >= 1, "n=0");
@@ -784,9 +784,19 @@ int fc_weighted_sum_dense(const float* const* rows, const float* w, int m, uint6
   uint64_t blocks = (nq + kBlock - 1) / kBlock;
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(k_wsum, dim3((uint32_t)blocks), dim3(kBlock), 0, (hipStream_t)stream, rows,
-                     w, m, n, out);
+                     w, m, n, out, acc_in);
   FC_LAUNCHED("k_wsum");
   return FC_OK;
+}
+
+int fc_weighted_sum_dense(const float* const* rows, const float* w, int m, uint64_t n,
+                          float* out, fc_stream_t stream) {
+  return weighted_sum_dense(rows, w, m, n, out, 0, stream);
+}
+
+int fc_weighted_sum_dense_continue(const float* const* rows, const float* w, int m, uint64_t n,
+                                   float* out, fc_stream_t stream) {
+  return weighted_sum_dense(rows, w, m, n, out, 1, stream);
 }
 
 // ---- float64 gradients (attack_models.py:105-106 -> aggregation.py:61) -------------------

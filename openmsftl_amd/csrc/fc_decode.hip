@@ -927,13 +927,23 @@ __global__ __launch_bounds__(kQBlock, 4) void k_fold_q(DecodeArgs a) {
 }
 
 // Dense FedAVG over M row pointers (gar.py:44 with 'full' rows): one float4 per thread.
+// acc_in: continue the row-order sum already in `out` (rows streamed in groups).
 __global__ __launch_bounds__(kBlock) void k_wsum(const float* const* rows, const float* w,
-                                                 int m, uint64_t n, float* out) {
+                                                 int m, uint64_t n, float* out, int acc_in) {
   const uint64_t nq = (n + 3) / 4;
   const uint64_t stride = (uint64_t)gridDim.x * kBlock;
   for (uint64_t q = (uint64_t)blockIdx.x * kBlock + threadIdx.x; q < nq; q += stride) {
     const uint64_t e = q * 4;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (acc_in) {
+      if (e + 4 <= n) {
+        acc = *reinterpret_cast<const float4*>(out + e);
+      } else {
+        acc.x = e + 0 < n ? out[e + 0] : 0.f;
+        acc.y = e + 1 < n ? out[e + 1] : 0.f;
+        acc.z = e + 2 < n ? out[e + 2] : 0.f;
+      }
+    }
     for (int r = 0; r < m; ++r) {
       const float* row = rows[r];
       float4 x;

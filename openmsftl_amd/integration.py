@@ -30,9 +30,12 @@ import sys
 from . import aggregation, compression, gar
 
 
-def install(aggregator: bool = True):
+def install(aggregator: bool = True, devices=None):
     """Swap the codec (and by default the aggregator's hot path) into ``ftl``.  Returns the
-    patched ``ftl.gradient_aggregation.aggregation`` module (or None with aggregator=False)."""
+    patched ``ftl.gradient_aggregation.aggregation`` module (or None with aggregator=False).
+    ``devices``: the GPUs the streamed aggregation fans out over when an aggregator's config
+    names none ("all", a count or a list of indices; None = the current device only)."""
+    aggregation.DEFAULT_DEVICES = devices
     sys.modules["ftl.compression"] = compression                  # experiment.py:7
     sys.modules["ftl.compression.compression"] = compression      # client.py:8
     for name in ("ftl.agents.client", "ftl.experiment"):          # already imported: re-point

@@ -25,6 +25,15 @@ whatever the client count (:func:`plan_group` sizes ``group`` for a byte budget)
 ``Aggregator.aggregate_grads`` (openmsftl_amd/aggregation.py) runs any number of sampled
 clients through it.
 
+Every codec of compression.py streams (:class:`RowCodec` per row of G, a :class:`RowPlan` for
+the round): ``'top'`` and native ``'rand'`` rows are ``fc_topk_encode`` packets, ``'rand'`` with
+the host permutation and ``'dropout-*'`` rows are ``fc_mask_encode`` idx/val packets (the mask
+drawn on the host from the global ``np.random`` in row order, or Philox Bernoulli on the
+device), and ``'full'`` rows are the gradient itself, copied H2D straight into the group's
+packet value buffer and folded by ``fc_weighted_sum_dense_continue``.  A group's rows are folded
+in row order, runs of packets by ``fc_decode_accumulate`` and runs of dense rows by the dense
+sum, each continuing the running aggregate: one left-to-right fp32 fold (gar.py:44).
+
 More than one GPU, still bit-exact (:class:`DeviceRing` in one process, :class:`RankRing`
 across processes): the fold groups — rows ``[t*group, (t+1)*group)`` of G — are dealt to the
 devices round-robin, and the running aggregate travels device to device in group order.  Each
@@ -39,8 +48,10 @@ tests/test_fullsize_parity.py / tests/test_e2e_multirank.py (the configs[4] dige
 """
 from __future__ import annotations
 
+import ctypes
 import threading
 from concurrent.futures import ThreadPoolExecutor
+from dataclasses import dataclass
 from typing import Callable, List, Optional, Sequence, Union
 
 import numpy as np
@@ -76,6 +87,166 @@ def group_bounds(clients: int, group: int) -> List[range]:
     return [range(g0, min(g0 + group, clients)) for g0 in range(0, clients, group)]
 
 
+@dataclass(frozen=True)
+class RowCodec:
+    """How one row of G is made on the device from its client's gradient (compression.py:23-77).
+
+    kind "top": fc_topk_encode packet of the k largest keys (``key_mode`` MAGNITUDE = 'top',
+    PHILOX = native 'rand' keyed by ``seed``/``offset``); "mask": fc_mask_encode idx/val packet
+    of codec ``codec`` (FC_CODEC_RAND / DROPOUT_*) with ``mask_src`` "host" (bits drawn on the
+    host, :meth:`RowPlan.take_mask`), "philox" (device Bernoulli(p)) or "none" (nothing kept:
+    'top' with k = 0); "dense": the gradient itself ('full', or 'top' with k = n)."""
+    kind: str
+    k: int = 0
+    key_mode: int = 0
+    seed: int = 0
+    offset: int = 0
+    codec: int = 0
+    p: float = 0.0
+    mask_src: str = "none"
+
+
+class RowPlan:
+    """The row codecs of one round, and the host RNG draws of its 'rand' / 'dropout-*' rows.
+
+    ``draws[i]()`` returns row i's mask as little-endian uint32 words (ceil(n/32)); the draws run
+    on ONE producer thread in increasing row order — the order in which the reference's loop
+    (aggregation.py:61-63) consumes the process-global ``np.random`` stream — at most
+    ``lookahead`` rows ahead of the pipeline, into pinned buffers that the pipeline copies H2D.
+    Several pipeline threads (:class:`DeviceRing`) may take masks; the draw order never
+    changes.  :meth:`close` waits for the producer (every draw done: the RNG is then where the
+    reference leaves it) and re-raises a draw's exception (e.g. NumPy's ValueError for p > 1)."""
+
+    def __init__(self, n: int, specs: Sequence[RowCodec], draws: Optional[dict] = None,
+                 lookahead: int = 8, base: int = 0, parent: "RowPlan" = None):
+        self.n, self.specs, self.base = n, specs, base
+        self._root = parent if parent is not None else self
+        if parent is not None:
+            return
+        self.draws = dict(draws or {})
+        self.nwords = (n + 31) // 32
+        self._cv = threading.Condition()
+        self._ready = {}
+        self._free = []
+        self._pool = max(1, min(int(lookahead), len(self.draws)))
+        self._made = 0
+        self._err = None
+        self._stop = False
+        self._thread = None
+        self._started = False
+        self._keep = None
+
+    def restrict(self, keep) -> None:
+        """Only rows with ``keep(i)`` will be taken (a rank's own rows): the others are still
+        drawn, in order, and dropped.  Call before the first :meth:`take_mask`."""
+        if self._root._started:
+            raise RuntimeError("restrict() after the draws started")
+        self._root._keep = keep
+
+    def _start(self) -> None:
+        r = self._root
+        with r._cv:
+            if r._started or not r.draws:
+                r._started = True
+                return
+            r._started = True
+            r._thread = threading.Thread(target=r._produce, name="fc-row-draws", daemon=True)
+            r._thread.start()
+
+    def __call__(self, i: int) -> RowCodec:
+        return self.specs[self.base + i]
+
+    def __len__(self) -> int:
+        return len(self.specs) - self.base
+
+    def shifted(self, start: int) -> "RowPlan":
+        """The plan of rows [start, ...) re-indexed from 0 (a merge cluster's rows)."""
+        return RowPlan(self.n, self.specs, base=self.base + start, parent=self._root)
+
+    # ---- producer -----------------------------------------------------------------------
+    def _buffer(self):
+        with self._cv:
+            while not self._free and self._made >= self._pool and not self._stop:
+                self._cv.wait()
+            if self._stop:
+                return None
+            if self._free:
+                return self._free.pop()
+            self._made += 1
+        buf = torch.empty(self.nwords, dtype=torch.int32)
+        return (buf.pin_memory() if torch.cuda.is_available() else buf), None
+
+    def _produce(self) -> None:
+        for i in sorted(self.draws):
+            if self._keep is not None and not self._keep(i):
+                try:
+                    self.draws[i]()                  # consumed from the RNG stream, not used
+                except BaseException as e:
+                    with self._cv:
+                        self._err = (i, e)
+                        self._cv.notify_all()
+                    return
+                continue
+            got = self._buffer()
+            if got is None:
+                return
+            buf, ev = got
+            if ev is not None:
+                ev.synchronize()                     # its previous H2D has read it
+            try:
+                words = self.draws[i]()
+                np.copyto(buf.numpy().view(np.uint32), words)
+            except BaseException as e:               # raised to the pipeline at row i
+                with self._cv:
+                    self._err = (i, e)
+                    self._cv.notify_all()
+                return
+            with self._cv:
+                self._ready[i] = buf
+                self._cv.notify_all()
+
+    # ---- consumers ----------------------------------------------------------------------
+    def take_mask(self, i: int) -> torch.Tensor:
+        """Row i's pinned mask words (blocks until drawn); hand the buffer back with
+        :meth:`release` once a copy from it has been queued."""
+        r, row = self._root, self.base + i
+        r._start()
+        with r._cv:
+            while row not in r._ready:
+                if r._err is not None and r._err[0] <= row:
+                    raise r._err[1]
+                if r._stop:
+                    raise RuntimeError("row plan closed")
+                r._cv.wait()
+            return r._ready.pop(row)
+
+    def release(self, buf: torch.Tensor, event) -> None:
+        r = self._root
+        with r._cv:
+            r._free.append((buf, event))
+            r._cv.notify_all()
+
+    def close(self, wait: bool = True) -> None:
+        """wait=True: every draw has run (raises the first draw error); False: stop early."""
+        r = self._root
+        if wait:
+            r._start()
+        if r._thread is not None:
+            if not wait:
+                with r._cv:
+                    r._stop = True
+                    r._cv.notify_all()
+            r._thread.join()
+            r._thread = None
+        if wait and r._err is not None:
+            raise r._err[1]
+
+
+def top_plan(n: int, k: int, clients: int) -> RowPlan:
+    """Every row a magnitude top-k packet (the configured codec, client_config.json:48-50)."""
+    return RowPlan(n, [RowCodec("top", k=k)] * clients)
+
+
 def _getter(host: HostSource):
     return host if callable(host) else (lambda i: host[i])
 
@@ -90,15 +261,17 @@ def _weights(clients: int, weights) -> np.ndarray:
 
 
 class HostFedAvg:
-    """A reusable H2D -> encode -> fold -> D2H pipeline for clients of length n, top-k k.
+    """A reusable H2D -> encode -> fold -> D2H pipeline for clients of length n.
 
-    ``sets`` packet sets of ``group`` packets each: with 2, one group encodes into one set
-    while the previous group, in the other, waits for the running aggregate (the rings)."""
+    Rows are made as their :class:`RowCodec` says (``plan`` of :meth:`run`; without one every
+    row is a top-k packet of ``k``).  ``sets`` packet sets of ``group`` packets each: with 2,
+    one group encodes into one set while the previous group, in the other, waits for the
+    running aggregate (the rings).  A dense row ('full') occupies its packet's value buffer."""
 
-    def __init__(self, n: int, k: int, *, group: int = 64, ring: int = 4, stage: int = 2,
-                 copy_threads: int = 4, pin: str = "stage",
+    def __init__(self, n: int, k: Optional[int] = None, *, group: int = 64, ring: int = 4,
+                 stage: int = 2, copy_threads: int = 4, pin: str = "stage",
                  device: Optional[torch.device] = None, sets: int = 1):
-        if not 0 < k < n:
+        if k is not None and not 0 < k < n:
             raise ValueError("HostFedAvg needs 0 < k < n")
         if pin not in ("stage", "register"):
             raise ValueError("pin must be 'stage' or 'register'")
@@ -110,12 +283,14 @@ class HostFedAvg:
         self.slots = [torch.empty(n, dtype=torch.float32, device=self.dev) for _ in range(ring)]
         self.hdrs = [torch.empty((group, L.HDR_BYTES), dtype=torch.uint8, device=self.dev)
                      for _ in range(sets)]
-        self.pktsets = [[codec.Packet.alloc(n, L.FC_FMT_IDXVAL, self.dev, hdr=h[j], k=k)
+        self.pktsets = [[codec.Packet.alloc(n, L.FC_FMT_IDXVAL, self.dev, hdr=h[j], k=k or 0)
                          for j in range(group)] for h in self.hdrs]
         self.pkts = self.pktsets[0]
         self.status_host = [torch.empty((group, 4), dtype=torch.uint8).pin_memory()
                             for _ in range(sets)]
         self.encoded = [torch.cuda.Event() for _ in range(sets)]
+        self.set_free = [torch.cuda.Event() for _ in range(sets)]   # the set's last fold read it
+        self.rows_of = [None] * sets                # (row codecs) of the group encoded in a set
         self.acc = torch.empty(n, dtype=torch.float32, device=self.dev)
         self.scratch = torch.empty(n, dtype=torch.float32, device=self.dev)
         self.out_host = torch.empty(n, dtype=torch.float32).pin_memory()
@@ -123,6 +298,8 @@ class HostFedAvg:
         self.h2d_done = [torch.cuda.Event() for _ in range(ring)]
         self.enc_done = [torch.cuda.Event() for _ in range(ring)]
         self._slot = 0
+        self.mslots = None                          # host-drawn mask words per ring slot
+        self.zero_mask = None
         # pinned staging for pageable sources (allocated on first use)
         self.nstage = max(1, stage)
         self.stage_bufs = None
@@ -133,6 +310,11 @@ class HostFedAvg:
         self._views = {}
         self.exact_fallbacks = 0
         self.staged_copies = 0
+
+    def _default_plan(self, clients: int) -> RowPlan:
+        if self.k is None:
+            raise ValueError("no row plan and no default k")
+        return top_plan(self.n, self.k, clients)
 
     # ---- host side ------------------------------------------------------------------
     def _as_cpu_tensor(self, src) -> torch.Tensor:
@@ -175,18 +357,21 @@ class HostFedAvg:
                 keep.append((ptr, ev, ref))
         self._registered = keep
 
-    def _h2d(self, src, slot: int) -> None:
-        """Queue one client's gradient into device slot ``slot`` on the copy stream."""
+    def _h2d(self, src, dst: torch.Tensor, wait=None, done=None) -> None:
+        """Queue one client's gradient into the device buffer ``dst`` on the copy stream, after
+        event ``wait`` (the buffer's previous reader); record ``done`` after the copy."""
         t = self._as_cpu_tensor(src)
-        self.copy.wait_event(self.enc_done[slot])
+        if wait is not None:
+            self.copy.wait_event(wait)
         if not t.is_pinned():
             if self.pin == "register" and self._register(t):
                 with torch.cuda.stream(self.copy):
-                    self.slots[slot].copy_(t, non_blocking=True)
+                    dst.copy_(t, non_blocking=True)
                     ev = torch.cuda.Event()
                     ev.record(self.copy)
                 self._registered.append((t.data_ptr(), ev, t))
-                self.h2d_done[slot].record(self.copy)
+                if done is not None:
+                    done.record(self.copy)
                 self._release_registered()
                 return
             if self.stage_bufs is None:
@@ -200,21 +385,52 @@ class HostFedAvg:
             self._host_copy(self.stage_bufs[b], t)
             t = self.stage_bufs[b]
             with torch.cuda.stream(self.copy):
-                self.slots[slot].copy_(t, non_blocking=True)
+                dst.copy_(t, non_blocking=True)
                 self.stage_free[b].record(self.copy)
         else:
             with torch.cuda.stream(self.copy):
-                self.slots[slot].copy_(t, non_blocking=True)
-        self.h2d_done[slot].record(self.copy)
+                dst.copy_(t, non_blocking=True)
+        if done is not None:
+            done.record(self.copy)
 
-    def _views_for(self, weights: np.ndarray, rows: range, ps: int) -> torch.Tensor:
-        key = (weights.tobytes(), rows.start, len(rows), ps)
+    def _mask_slot(self, slot: int, plan: RowPlan, i: int) -> torch.Tensor:
+        """Row i's host-drawn mask into the ring slot's device mask words (copy stream, after
+        the slot's previous encode: queue it after :meth:`_h2d` of the same slot)."""
+        if self.mslots is None:
+            words = (self.n + 31) // 32
+            self.mslots = [torch.empty(words, dtype=torch.int32, device=self.dev)
+                           for _ in range(self.ring)]
+        buf = plan.take_mask(i)
+        with torch.cuda.stream(self.copy):
+            self.mslots[slot].copy_(buf, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self.copy)
+        plan.release(buf, ev)
+        return self.mslots[slot]
+
+    def _views_for(self, weights: np.ndarray, rows: range, ps: int, j0: int = 0) -> torch.Tensor:
+        key = ("v", weights.tobytes(), rows.start, len(rows), ps, j0)
         v = self._views.get(key)
         if v is None:
-            v = codec.views_tensor(self.pktsets[ps][:len(rows)],
+            v = codec.views_tensor(self.pktsets[ps][j0:j0 + len(rows)],
                                    [float(x) for x in weights[rows.start:rows.stop]], self.dev)
-            self._views = {key: v} if len(self._views) > 64 else {**self._views, key: v}
+            self._cache(key, v)
         return v
+
+    def _dense_args(self, weights: np.ndarray, rows: range, ps: int, j0: int):
+        """(row pointers, weights) device arrays of a run of dense rows held in the set's
+        packet value buffers."""
+        key = ("d", weights.tobytes(), rows.start, len(rows), ps, j0)
+        v = self._views.get(key)
+        if v is None:
+            ptrs = [p.val.data_ptr() for p in self.pktsets[ps][j0:j0 + len(rows)]]
+            v = (torch.tensor(ptrs, dtype=torch.int64).to(self.dev),
+                 torch.from_numpy(np.ascontiguousarray(weights[rows.start:rows.stop])).to(self.dev))
+            self._cache(key, v)
+        return v
+
+    def _cache(self, key, v) -> None:
+        self._views = {key: v} if len(self._views) > 64 else {**self._views, key: v}
 
     # ---- one fold group (rows of G) ---------------------------------------------------
     def begin(self) -> None:
@@ -223,37 +439,70 @@ class HostFedAvg:
         for e in self.enc_done:
             e.record(comp)
 
-    def encode_group(self, get, rows: range, ps: int = 0) -> None:
+    def encode_group(self, get, rows: range, ps: int = 0, plan: Optional[RowPlan] = None) -> None:
         """Queue H2D + encode of ``rows`` into packet set ``ps`` on the current stream, then
         the copy of their status words to pinned host memory (:meth:`check_group` reads
-        them; the host does not wait here)."""
+        them; the host does not wait here).  Dense rows are copied straight into their
+        packet's value buffer (after the set's previous fold, ``set_free``)."""
         if len(rows) > self.group:
             raise ValueError(f"a fold group holds at most {self.group} rows")
+        plan = plan if plan is not None else self._default_plan(rows.stop)
         comp = torch.cuda.current_stream(self.dev)
         pk = self.pktsets[ps]
-        for j, i in enumerate(rows):
+        specs = [plan(i) for i in rows]
+        dense_h2d = None
+        for j, (i, rc) in enumerate(zip(rows, specs)):
+            if rc.kind == "dense":
+                if dense_h2d is None:
+                    dense_h2d = torch.cuda.Event()
+                    self.copy.wait_event(self.set_free[ps])
+                self._h2d(get(i), pk[j].val[:self.n])
+                continue
             s = self._slot
             self._slot = (s + 1) % self.ring
-            self._h2d(get(i), s)
+            self._h2d(get(i), self.slots[s], wait=self.enc_done[s])
+            mask = self._mask_slot(s, plan, i) if rc.mask_src == "host" else None
+            self.h2d_done[s].record(self.copy)
             comp.wait_event(self.h2d_done[s])
-            codec.encode_top(self.slots[s], self.k, packet=pk[j], check=False)
+            if rc.kind == "top":
+                codec.encode_top(self.slots[s], rc.k, key_mode=rc.key_mode, seed=rc.seed,
+                                 offset=rc.offset, packet=pk[j], check=False)
+            elif rc.kind == "mask":
+                if rc.mask_src == "none":
+                    if self.zero_mask is None:
+                        self.zero_mask = torch.zeros((self.n + 31) // 32, dtype=torch.int32,
+                                                     device=self.dev)
+                    mask = self.zero_mask
+                codec.encode_mask(self.slots[s], rc.codec, p=rc.p, mask_bits=mask, seed=rc.seed,
+                                  offset=rc.offset, fmt=L.FC_FMT_IDXVAL, packet=pk[j])
+            else:
+                raise ValueError(f"unknown row kind {rc.kind!r}")
             self.enc_done[s].record(comp)
+        if dense_h2d is not None:
+            dense_h2d.record(self.copy)
+            comp.wait_event(dense_h2d)
+        self.rows_of[ps] = specs
         m = len(rows)
         self.status_host[ps][:m].copy_(self.hdrs[ps][:m, 36:40], non_blocking=True)
         self.encoded[ps].record(comp)
 
     def check_group(self, get, rows: range, ps: int = 0) -> torch.cuda.Event:
-        """Wait for the group's status words; a packet whose sampled bracket missed is
+        """Wait for the group's status words; a top-k packet whose sampled bracket missed is
         re-encoded exactly from its host copy (current stream).  Returns an event after
-        which the group's packets are final."""
+        which the group's rows are final."""
         self.encoded[ps].synchronize()
+        specs = self.rows_of[ps]
         st = self.status_host[ps][:len(rows)].numpy().view(np.uint32).ravel()
-        bad = np.nonzero(st)[0]
-        if len(bad) == 0:
+        bad = [int(j) for j in np.nonzero(st)[0] if specs[int(j)].kind != "dense"]
+        if not bad:
             return self.encoded[ps]
         for j in bad:
-            self.scratch.copy_(self._as_cpu_tensor(get(rows.start + int(j))))
-            codec.encode_top(self.scratch, self.k, packet=self.pktsets[ps][int(j)], exact=True)
+            rc = specs[j]
+            if rc.kind != "top" or st[j] != L.FC_STATUS_RETRY_EXACT:
+                raise L.FedCodecError(f"row {rows.start + j}: packet status {int(st[j])}")
+            self.scratch.copy_(self._as_cpu_tensor(get(rows.start + j)))
+            codec.encode_top(self.scratch, rc.k, key_mode=rc.key_mode, seed=rc.seed,
+                             offset=rc.offset, packet=self.pktsets[ps][j], exact=True)
             self.exact_fallbacks += 1
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(self.dev))
@@ -261,10 +510,32 @@ class HostFedAvg:
 
     def fold_group(self, weights: np.ndarray, rows: range, ps: int, acc: torch.Tensor,
                    continue_sum: bool) -> None:
-        """acc (+)= the group's rows in order (fc_decode_accumulate[_continue]), current stream."""
-        codec.decode_accumulate(self.pktsets[ps][:len(rows)], None, out=acc,
-                                views=self._views_for(weights, rows, ps),
-                                continue_sum=continue_sum)
+        """acc (+)= the group's rows in row order, current stream: each run of packets by
+        fc_decode_accumulate[_continue], each run of dense rows by
+        fc_weighted_sum_dense[_continue] (the same left-to-right fp32 sum, gar.py:44)."""
+        lib = L.load()
+        specs = self.rows_of[ps]
+        stream = codec._stream(self.dev)
+        j = 0
+        while j < len(rows):
+            dense = specs[j].kind == "dense"
+            j1 = j + 1
+            while j1 < len(rows) and (specs[j1].kind == "dense") == dense:
+                j1 += 1
+            sub = range(rows.start + j, rows.start + j1)
+            cont = continue_sum or j > 0
+            if dense:
+                ptrs, w = self._dense_args(weights, sub, ps, j)
+                fn = lib.fc_weighted_sum_dense_continue if cont else lib.fc_weighted_sum_dense
+                L.check(fn(ctypes.c_void_p(ptrs.data_ptr()), ctypes.c_void_p(w.data_ptr()),
+                           len(sub), self.n, ctypes.c_void_p(acc.data_ptr()), stream),
+                        "fc_weighted_sum_dense")
+            else:
+                codec.decode_accumulate(self.pktsets[ps][j:j1], None, out=acc,
+                                        views=self._views_for(weights, sub, ps, j),
+                                        continue_sum=cont)
+            j = j1
+        self.set_free[ps].record(torch.cuda.current_stream(self.dev))
 
     def finish(self) -> None:
         if self._registered:
@@ -273,16 +544,19 @@ class HostFedAvg:
     # ---- one device, sequential groups -----------------------------------------------
     def run(self, host: HostSource, clients: int, weights: Optional[np.ndarray] = None,
             sync: bool = True, out: Optional[torch.Tensor] = None,
-            to_host: bool = True, continue_sum: bool = False) -> torch.Tensor:
+            to_host: bool = True, continue_sum: bool = False,
+            plan: Optional[RowPlan] = None) -> torch.Tensor:
         """FedAVG of ``clients`` host gradients (``host[i]`` or ``host(i)``: fp32 CPU tensors
         or NumPy arrays of n elements; pinned ones are copied directly) with float32 weights
-        (default fl32(1/M), gar.py:37-40).  Returns the pinned host aggregate (valid after the
-        stream syncs; ``sync`` does it), or with ``to_host=False`` the device aggregate
-        (``out`` if given: a float32 CUDA tensor of n elements).  ``continue_sum``: ``out``
-        already holds the left-to-right sum of earlier rows (another device's or rank's shard)
-        and these rows continue it, so a chain of runs is one fold over all rows (gar.py:44)."""
+        (default fl32(1/M), gar.py:37-40), row i made as ``plan(i)`` says (default: top-k of
+        ``k``).  Returns the pinned host aggregate (valid after the stream syncs; ``sync``
+        does it), or with ``to_host=False`` the device aggregate (``out`` if given: a float32
+        CUDA tensor of n elements).  ``continue_sum``: ``out`` already holds the left-to-right
+        sum of earlier rows (another device's or rank's shard) and these rows continue it, so
+        a chain of runs is one fold over all rows (gar.py:44)."""
         get = _getter(host)
         w = _weights(clients, weights)
+        plan = plan if plan is not None else self._default_plan(clients)
         acc = self.acc if out is None else out
         if acc.dtype != torch.float32 or acc.numel() != self.n or not acc.is_cuda:
             raise ValueError("out must be a float32 CUDA tensor of n elements")
@@ -290,7 +564,7 @@ class HostFedAvg:
             raise ValueError("continue_sum needs the running sum in out")
         self.begin()
         for rows in group_bounds(clients, self.group):
-            self.encode_group(get, rows, 0)
+            self.encode_group(get, rows, 0, plan)
             self.check_group(get, rows, 0)
             self.fold_group(w, rows, 0, acc, continue_sum or rows.start > 0)
         if clients == 0 and not continue_sum:
@@ -304,7 +578,7 @@ class HostFedAvg:
         return self.out_host
 
 
-def host_fold(pipe: HostFedAvg, host: HostSource):
+def host_fold(pipe: HostFedAvg, host: HostSource, plan: Optional[RowPlan] = None):
     """A :data:`openmsftl_amd.distributed.Fold` over host gradients: the rows ``rows`` of G
     (global client indices, ``host[i]`` / ``host(i)``) streamed through ``pipe`` into the
     device partial sum ``out``.  Composes the host-resident round (configs[4]) with
@@ -315,13 +589,14 @@ def host_fold(pipe: HostFedAvg, host: HostSource):
     def fold(rows: range, w: np.ndarray, out, continue_sum: bool):
         r0 = rows.start
         return pipe.run(lambda j: get(r0 + j), len(rows), np.asarray(w, np.float32), sync=False,
-                        out=out, to_host=False, continue_sum=continue_sum)
+                        out=out, to_host=False, continue_sum=continue_sum,
+                        plan=plan.shifted(r0) if plan is not None else None)
     return fold
 
 
 # ---- the running aggregate travels between devices in group order -------------------------
 def _ring_worker(pipe: HostFedAvg, get, w: np.ndarray, groups: List[range], mine: List[int],
-                 acc: torch.Tensor, comp, fold_s, take, give) -> None:
+                 acc: torch.Tensor, comp, fold_s, take, give, plan: RowPlan) -> None:
     """One device's share of a ring round: its groups ``mine`` (indices into ``groups``,
     increasing).  Group t's successor on this device encodes into the other packet set while
     group t waits for the aggregate of the rows before it: ``take(t)`` (called with the fold
@@ -355,7 +630,7 @@ def _ring_worker(pipe: HostFedAvg, get, w: np.ndarray, groups: List[range], mine
             ps = idx % pipe.sets
             if done[ps] is not None:
                 comp.wait_event(done[ps])             # the set's previous group is folded
-            pipe.encode_group(get, groups[t], ps)
+            pipe.encode_group(get, groups[t], ps, plan)
             if pending is not None:
                 finish(*pending)
             pending = (t, ps)
@@ -397,12 +672,19 @@ class DeviceRing:
         return sum(p.exact_fallbacks for p in self.pipes)
 
     def run(self, host: HostSource, clients: int, weights: Optional[np.ndarray] = None,
-            to_host: bool = True) -> torch.Tensor:
-        """The FedAVG aggregate of ``clients`` host gradients: the pinned host array (synced),
-        or with ``to_host=False`` the device tensor holding it (on the last group's device,
-        ordered before later work on that device's current stream)."""
+            to_host: bool = True, plan: Optional[RowPlan] = None) -> torch.Tensor:
+        """The FedAVG aggregate of ``clients`` host gradients (row i made as ``plan(i)`` says,
+        default top-k of ``k``): the pinned host array (synced), or with ``to_host=False`` the
+        device tensor holding it (on the last group's device, ordered before later work on
+        that device's current stream; the next run writes it only after the work the caller
+        has queued on its devices' current streams by then)."""
         get = _getter(host)
         w = _weights(clients, weights)
+        plan = plan if plan is not None else self.pipes[0]._default_plan(clients)
+        for d, p in enumerate(self.pipes):       # the last run's result may still be read there
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(p.dev))
+            self.fold[d].wait_event(ev)
         groups = group_bounds(clients, self.group)
         D = len(self.pipes)
         if not groups:
@@ -431,7 +713,7 @@ class DeviceRing:
                 mine = list(range(d, len(groups), D))
                 if mine:
                     _ring_worker(self.pipes[d], get, w, groups, mine, self.accs[d],
-                                 self.comp[d], self.fold[d], take, give)
+                                 self.comp[d], self.fold[d], take, give, plan)
             except BaseException:
                 with cv:
                     failed.append(d)
@@ -491,12 +773,17 @@ class RankRing:
         else:
             dist.recv(t, src=peer, group=self.pg)
 
-    def run(self, host: HostSource, clients: int, weights: Optional[np.ndarray] = None
-            ) -> Optional[torch.Tensor]:
+    def run(self, host: HostSource, clients: int, weights: Optional[np.ndarray] = None,
+            plan: Optional[RowPlan] = None) -> Optional[torch.Tensor]:
         """Returns the device aggregate on ``dst`` (ordered before later work on the current
-        stream), None on the other ranks.  ``host(i)`` is called for this rank's rows only."""
+        stream), None on the other ranks.  ``host(i)`` is called for this rank's rows only.
+        A ``plan`` with host draws must be the same on every rank (each rank draws every
+        row's mask in order, so all ranks leave the RNG where the reference does)."""
         get = _getter(host)
         w = _weights(clients, weights)
+        plan = plan if plan is not None else self.pipe._default_plan(clients)
+        G_, W_, r_ = self.pipe.group, self.world, self.rank
+        plan.restrict(lambda i: (i // G_) % W_ == r_)
         groups = group_bounds(clients, self.pipe.group)
         if not groups:
             raise Exception("Empty gradient list")               # aggregation.py:59-60
@@ -523,7 +810,8 @@ class RankRing:
 
         mine = list(range(r, len(groups), W))
         if mine:
-            _ring_worker(self.pipe, get, w, groups, mine, acc, self.comp, self.fold, take, give)
+            _ring_worker(self.pipe, get, w, groups, mine, acc, self.comp, self.fold, take, give,
+                         plan)
         cur = torch.cuda.current_stream(self.pipe.dev)
         if r == self.dst and last_owner != self.dst:
             with torch.cuda.device(self.pipe.dev), torch.cuda.stream(self.fold):

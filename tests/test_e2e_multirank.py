@@ -87,8 +87,8 @@ def test_device_ring_forced_retry_is_exact():
     pipes = _pipes(2, 2)
     orig = pipes[1].encode_group
 
-    def poked(get, rows, ps=0):
-        orig(get, rows, ps)
+    def poked(get, rows, ps=0, plan=None):
+        orig(get, rows, ps, plan)
         # after the status copy was queued: overwrite the pinned status of the group's first
         # client once the encode is done (check_group waits on the same event first)
         pipes[1].encoded[ps].synchronize()
@@ -194,7 +194,7 @@ def test_aggregator_fans_out_over_devices():
     agg = Aggregator({"aggregation_scheme": "fed_avg", "devices": [0, 0],
                       "device_budget_bytes": budget})
     agg.aggregate_grads([Client(i, g, C) for i, g in enumerate(grads)])
-    assert agg.agg_path == "stream-top"
+    assert agg.agg_path == "stream"
     (pipe,) = agg._host_pipelines.values()
     assert isinstance(pipe, DeviceRing) and len(pipe.pipes) == 2 and pipe.group < 11
     assert agg.agg_grad.tobytes() == want.tobytes()

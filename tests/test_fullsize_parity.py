@@ -137,7 +137,7 @@ def test_configs4_device_aggregator_70x25M(configs4_host, pin):
     agg._host_pipelines = {}
     agg.aggregate_grads(clients)                       # allocates the ring + packets
     agg._host_pipelines[next(iter(agg._host_pipelines))].pin = pin
-    assert agg.agg_path == "stream-top"
+    assert agg.agg_path == "stream"
     assert sha(agg.agg_grad) == d["aggregate_sha256"], "configs4: Aggregator aggregate differs"
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -147,6 +147,43 @@ def test_configs4_device_aggregator_70x25M(configs4_host, pin):
     gbps = 4.0 * d["n"] * d["clients"] / dt / 1e9
     print(f"\n[configs4 Aggregator numpy->numpy pin={pin}] {dt:.3f} s = {gbps:.2f} GB/s "
           f"of client gradients")
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("codec_name,clients", [("full", 70), ("dropout-unbiased", 16),
+                                                ("rand", 6)])
+def test_configs4_device_aggregator_other_codecs(configs4_host, codec_name, clients):
+    """The Aggregator's streamed path for the other codecs at the configs[4] size (25.5 M):
+    'full' (the reference's configured codec, client_config.json:48) over all 70 clients,
+    'dropout-unbiased' p = 0.1 and 'rand' f = 0.01 (host masks drawn from np.random in row
+    order) over the first clients, with the default device budget; agg_grad byte-equal to the
+    oracle's row-order fold of the oracle's rows (compression.py:39-60, gar.py:44) and the
+    RNG where the reference leaves it.  Prints the NumPy-to-NumPy rate."""
+    import time
+
+    from oracle import compression_oracle as co
+    from oracle import gar_oracle as go
+    from openmsftl_amd import Compression
+    from openmsftl_amd.aggregation import Aggregator
+    cfg = {"compression_function": codec_name, "dropout_p": 0.1, "fraction_coordinate": 0.01}
+    grads = configs4_host[:clients]
+    w = np.full(clients, 1.0 / clients, np.float32)
+    np.random.seed(4)
+    want = go.sequential_weighted_sum((np.asarray(co.compress(cfg, g), np.float32) for g in grads), w)
+    nxt = int(np.random.randint(0, 2 ** 31 - 1))
+    agg = Aggregator({"aggregation_scheme": "fed_avg"})
+    C = Compression(cfg)
+    for rep in range(2):
+        np.random.seed(4)
+        t0 = time.perf_counter()
+        agg.aggregate_grads([_Client(i, g, C) for i, g in enumerate(grads)])
+        dt = time.perf_counter() - t0
+        assert agg.agg_path == "stream"
+        assert int(np.random.randint(0, 2 ** 31 - 1)) == nxt
+        assert agg.agg_grad.tobytes() == want.tobytes(), f"{codec_name}: aggregate differs"
+    gbps = 4.0 * D["configs4"]["n"] * clients / dt / 1e9
+    print(f"\n[configs4 Aggregator numpy->numpy {codec_name} x {clients}] {dt:.3f} s = "
+          f"{gbps:.2f} GB/s of client gradients")
 
 
 @pytest.mark.timeout(300)

@@ -892,7 +892,7 @@ def test_aggregator_top_packets_match_dense_reference(sizes):
                       "cluster_size_list": sizes,
                       "device_budget_bytes": 6 * 4 * n + 3 * packet_bytes(n) + (8 << 20)})
     agg.aggregate_grads(clients)
-    assert agg.agg_path == "stream-top"                # the streamed packet path ran
+    assert agg.agg_path == "stream"                # the streamed packet path ran
     Gd = go.build_dense_G([co.compress(cfg, x) for x in grads], np.float32)
     for cs in sizes:
         Gd = go.merge_gradient(Gd, cs)

@@ -104,7 +104,7 @@ def test_device_aggregator_configs0_round(name):
     np.random.seed(r["seed"])
     agg.aggregate_grads([_Client(i, g, C) for i, g in enumerate(grads)])
     assert int(np.random.randint(0, 2 ** 31 - 1)) == r["rng_next"]
-    assert agg.agg_path == ("stream-top" if name == "top" else "dense")
+    assert agg.agg_path == "stream"                  # every configs[0] codec streams
     assert str(agg.agg_grad.dtype) == r["agg_dtype"]
     assert sha(agg.agg_grad) == r["agg_grad"]
     if agg.curr_G is not None:

@@ -1,0 +1,330 @@
+"""Every codec through the streamed Aggregator.
+
+``Aggregator.aggregate_grads`` (aggregation.py:54-78) builds G row by row from
+``client.C.compress(client.grad)`` (compression.py:23-77) and reduces it (gar.py:44).  The
+device path streams every fp32 codec instead — 'full' as dense rows, 'top' / native 'rand' as
+top-k packets, 'rand' / 'dropout-*' as mask packets whose masks the host draws from the global
+``np.random`` in row order — with device memory bounded by ``device_budget_bytes``.
+
+CPU tests: the row plan (which rows become what, the host draws in row order, the RNG left
+where the reference's loop leaves it, errors at the reference's row).  GPU tests: agg_grad
+byte-equal to the oracle's FedAVG of the oracle's G (compression_oracle / gar_oracle, the
+checker only), with a budget far below M x N, and the RNG state after the round equal to the
+reference's."""
+import numpy as np
+import pytest
+
+from oracle import compression_oracle as co
+from oracle import gar_oracle as go
+
+N = 100_003                                   # ragged: the last chunk is partial
+M = 16
+
+
+class _Client:
+    """The attributes aggregation.py:59-66 reads from a client."""
+
+    def __init__(self, cid, grad, C):
+        self.client_id, self.grad, self.C = cid, grad, C
+
+
+class _RefCompression:
+    """A reference-shaped Compression (compression.py:18-21 attributes only, no 'rng')."""
+
+    def __init__(self, cfg):
+        self.compression_function = cfg.get("compression_function", "full")
+        self.num_bits = cfg.get("num_bits", 8)
+        self.fraction_coordinates = cfg.get("fraction_coordinate", 0.5)
+        self.dropout_p = cfg.get("dropout_p", 0.5)
+
+
+CFGS = {
+    "full": {"compression_function": "full"},
+    "top": {"compression_function": "top", "fraction_coordinate": 0.1},
+    "rand": {"compression_function": "rand", "fraction_coordinate": 0.1},
+    "dropout-biased": {"compression_function": "dropout-biased", "dropout_p": 0.1},
+    "dropout-unbiased": {"compression_function": "dropout-unbiased", "dropout_p": 0.1},
+}
+
+
+def _grads(m, n, seed):
+    rng = np.random.default_rng(seed)
+    return [(rng.standard_normal(n) * 10.0 ** rng.uniform(-4, -1)).astype(np.float32)
+            for _ in range(m)]
+
+
+def _reference_round(cfgs, grads, seed, sizes=()):
+    """aggregation.py:61-78 with the oracle codec: (agg_grad, next RNG draw)."""
+    np.random.seed(seed)
+    rows = [co.compress(c, g) for c, g in zip(cfgs, grads)]
+    nxt = int(np.random.randint(0, 2 ** 31 - 1))
+    G = go.build_dense_G(rows, np.float32)
+    for cs in sizes:
+        G = go.merge_gradient(G, cs)
+    return go.FedAvgOracle({}).aggregate(G), nxt
+
+
+# ---- CPU: the row plan ---------------------------------------------------------------------
+def test_row_plan_kinds():
+    from openmsftl_amd import Compression
+    from openmsftl_amd import _lib as L
+    from openmsftl_amd.aggregation import row_plan
+    n = 1000
+    cfgs = [CFGS["full"], CFGS["top"], CFGS["rand"], CFGS["dropout-biased"],
+            CFGS["dropout-unbiased"], {"compression_function": "top", "fraction_coordinate": 1.0},
+            {"compression_function": "top", "fraction_coordinate": 0.0},
+            {"compression_function": "top", "fraction_coordinate": -0.1},
+            {"compression_function": "rand", "fraction_coordinate": 0.1, "rng": "philox",
+             "seed": 7},
+            {"compression_function": "dropout-unbiased", "dropout_p": 0.3, "rng": "philox",
+             "seed": 9}]
+    clients = [_Client(i, np.zeros(n, np.float32), Compression(c)) for i, c in enumerate(cfgs)]
+    state = np.random.get_state()[1].copy()
+    plan = row_plan(clients, n)
+    assert (np.random.get_state()[1] == state).all()       # nothing drawn yet
+    kinds = [(r.kind, r.mask_src) for r in plan.specs]
+    assert kinds == [("dense", "none"), ("top", "none"), ("mask", "host"), ("mask", "host"),
+                     ("mask", "host"), ("dense", "none"), ("mask", "none"), ("top", "none"),
+                     ("top", "none"), ("mask", "philox")]
+    assert plan.specs[1].k == 100 and plan.specs[7].k == 900    # f < 0: the slice drops 100
+    assert plan.specs[8].key_mode == L.FC_KEY_PHILOX and plan.specs[8].seed == 7
+    assert plan.specs[8].offset == 1 and plan.specs[9].offset == 1 and plan.specs[9].p == 0.3
+    assert plan.specs[4].codec == L.FC_CODEC_DROPOUT_UNBIASED and plan.specs[4].p == 0.1
+    assert sorted(plan.draws) == [2, 3, 4]
+    plan.close()
+
+
+@pytest.mark.parametrize("cfg", [{"compression_function": "qsgd"},
+                                 {"compression_function": "nope"},
+                                 {"compression_function": "qsgd", "qsgd": "native"},
+                                 {"compression_function": "dropout-biased", "dropout_p": 2.0,
+                                  "rng": "philox"}])
+def test_row_plan_rejects_what_the_generic_path_must_raise(cfg):
+    from openmsftl_amd import Compression
+    from openmsftl_amd.aggregation import row_plan
+    clients = [_Client(0, np.zeros(10, np.float32), Compression(CFGS["top"])),
+               _Client(1, np.zeros(10, np.float32), Compression(cfg))]
+    assert row_plan(clients, 10) is None
+
+
+def test_row_plan_draws_in_row_order_and_leave_the_reference_rng():
+    """The producer thread's draws are the reference's draws (compression.py:43, :51, :58) in
+    row order: each mask equals the oracle's for the same RNG position, and the global RNG
+    ends where the reference's loop leaves it (reference-shaped Compression objects too)."""
+    from openmsftl_amd import Compression
+    from openmsftl_amd.aggregation import row_plan
+    from openmsftl_amd.compression import bitmask_words
+    n, seed = 4099, 1234
+    names = ["rand", "top", "dropout-biased", "full", "dropout-unbiased", "rand", "rand"]
+    cfgs = [CFGS[x] for x in names]
+    np.random.seed(seed)
+    want = {}
+    for i, c in enumerate(cfgs):
+        if c["compression_function"] == "rand":
+            want[i] = bitmask_words(co.draw_rand_indices(n, co.num_kept(0.1, n)), n, False)
+        elif c["compression_function"].startswith("dropout"):
+            want[i] = bitmask_words(co.draw_dropout_mask(n, c["dropout_p"]), n, True)
+    nxt = int(np.random.randint(0, 2 ** 31 - 1))
+    for mk in (Compression, _RefCompression):
+        np.random.seed(seed)
+        clients = [_Client(i, np.zeros(n, np.float32), mk(c)) for i, c in enumerate(cfgs)]
+        plan = row_plan(clients, n)
+        for i in sorted(want):
+            buf = plan.take_mask(i)
+            assert buf.numpy().view(np.uint32).tobytes() == want[i].tobytes(), (mk, i)
+            plan.release(buf, None)
+        plan.close()
+        assert int(np.random.randint(0, 2 ** 31 - 1)) == nxt
+
+
+def test_row_plan_restrict_and_shift():
+    """A rank takes only its own rows (restrict): the others are drawn and dropped, so the
+    RNG still ends where the reference leaves it; a shifted plan (a merge cluster) indexes
+    from its first row."""
+    from openmsftl_amd import Compression
+    from openmsftl_amd.aggregation import row_plan
+    n, seed = 777, 5
+    np.random.seed(seed)
+    want = [co.draw_dropout_mask(n, 0.3) for _ in range(9)]
+    nxt = int(np.random.randint(0, 2 ** 31 - 1))
+    from openmsftl_amd.compression import bitmask_words
+    np.random.seed(seed)
+    C = Compression({"compression_function": "dropout-biased", "dropout_p": 0.3})
+    plan = row_plan([_Client(i, np.zeros(n, np.float32), C) for i in range(9)], n)
+    plan.restrict(lambda i: i % 3 == 1)
+    sub = plan.shifted(4)
+    for i in (1, 4, 7):
+        buf = plan.take_mask(i) if i != 7 else sub.take_mask(3)
+        assert buf.numpy().view(np.uint32).tobytes() == bitmask_words(want[i], n, True).tobytes()
+        plan.release(buf, None)
+    plan.close()
+    assert int(np.random.randint(0, 2 ** 31 - 1)) == nxt
+
+
+def test_row_plan_draw_error_surfaces_at_its_row():
+    """np.random.binomial(1, 1.5, ...) raises ValueError at that row (compression.py:51), as
+    the reference's loop does; earlier rows' masks are intact."""
+    from openmsftl_amd.aggregation import row_plan
+    n = 100
+    clients = [_Client(0, np.zeros(n, np.float32), _RefCompression(CFGS["dropout-biased"])),
+               _Client(1, np.zeros(n, np.float32),
+                       _RefCompression({"compression_function": "dropout-biased",
+                                        "dropout_p": 1.5}))]
+    plan = row_plan(clients, n)
+    buf = plan.take_mask(0)
+    plan.release(buf, None)
+    with pytest.raises(ValueError):
+        plan.take_mask(1)
+    with pytest.raises(ValueError):
+        plan.close()
+
+
+# ---- GPU: the streamed Aggregator against the oracle ---------------------------------------
+def _budget(n, packets, sets=1):
+    """Device bytes for the ring (4 slots), the aggregate + scratch, one workspace and
+    ``packets`` packets per set (pipeline.plan_group's account)."""
+    from openmsftl_amd import _lib as L
+    from openmsftl_amd.pipeline import packet_bytes
+    return 6 * 4 * n + int(L.load().fc_workspace_bytes(n)) + sets * packets * packet_bytes(n)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", list(CFGS))
+@pytest.mark.parametrize("ref_objects", [False, True])
+def test_aggregator_streams_every_codec(name, ref_objects):
+    """agg_grad byte-equal to the reference round (oracle), M x N far above the device budget
+    (3 packets per fold group: 6 groups), the RNG state after the round equal."""
+    pytest.importorskip("torch")
+    from openmsftl_amd import Compression
+    from openmsftl_amd.aggregation import Aggregator
+    grads = _grads(M, N, seed=sorted(CFGS).index(name))
+    seed = 31
+    want, nxt = _reference_round([CFGS[name]] * M, grads, seed)
+    budget = _budget(N, 3)
+    assert budget < M * N * 4
+    mk = _RefCompression if ref_objects else Compression
+    agg = Aggregator({"aggregation_scheme": "fed_avg", "device_budget_bytes": budget})
+    np.random.seed(seed)
+    agg.aggregate_grads([_Client(i, g, mk(CFGS[name])) for i, g in enumerate(grads)])
+    assert int(np.random.randint(0, 2 ** 31 - 1)) == nxt
+    assert agg.agg_path == "stream" and agg.curr_G is None
+    (pipe,) = agg._host_pipelines.values()
+    assert pipe.group == 3
+    assert agg.agg_grad.dtype == np.float32
+    assert agg.agg_grad.tobytes() == want.tobytes()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sizes", [[], [4], [5, 2]])
+def test_aggregator_streams_mixed_codecs(sizes):
+    """One round mixing every codec (runs of dense rows and packets inside one fold group),
+    with hierarchical merges (aggregation.py:80-93) over the streamed rows; trivial top
+    fractions (k = n: dense, k = 0: nothing kept, f < 0: the slice)."""
+    pytest.importorskip("torch")
+    from openmsftl_amd import Compression
+    from openmsftl_amd.aggregation import Aggregator
+    names = ["full", "full", "top", "rand", "dropout-biased", "full", "dropout-unbiased",
+             "top", "top", "top", "rand", "full", "dropout-unbiased", "dropout-biased"]
+    cfgs = [CFGS[x] for x in names]
+    cfgs[8] = {"compression_function": "top", "fraction_coordinate": 1.0}
+    cfgs[9] = {"compression_function": "top", "fraction_coordinate": -0.25}
+    cfgs[7] = {"compression_function": "top", "fraction_coordinate": 0.0}
+    grads = _grads(len(cfgs), N, seed=77)
+    grads[1][::7] = -0.0
+    seed = 2024
+    want, nxt = _reference_round(cfgs, grads, seed, sizes)
+    agg = Aggregator({"aggregation_scheme": "fed_avg", "device_budget_bytes": _budget(N, 4),
+                      "num_hierarchies": len(sizes), "cluster_size_list": sizes})
+    np.random.seed(seed)
+    agg.aggregate_grads([_Client(i, g, Compression(c)) for i, (g, c) in enumerate(zip(grads, cfgs))])
+    assert int(np.random.randint(0, 2 ** 31 - 1)) == nxt
+    assert agg.agg_path == "stream"
+    assert agg.agg_grad.tobytes() == want.tobytes()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["rand", "dropout-biased", "dropout-unbiased"])
+def test_aggregator_streams_philox_modes_like_the_generic_path(name):
+    """Native RNG ('rng': 'philox'): the streamed rows equal the drop-in compress() rows of
+    Compression objects in the same state (the same Philox offsets, taken in row order)."""
+    torch = pytest.importorskip("torch")
+    from openmsftl_amd import Compression
+    from openmsftl_amd.aggregation import Aggregator
+    cfg = dict(CFGS[name], rng="philox", seed=11)
+    grads = _grads(9, N, seed=5)
+    Cs = [Compression(cfg) for _ in range(3)]               # shared objects: offsets advance
+    rows = [np.asarray(Cs[i % 3].compress(torch.from_numpy(g).cuda()).cpu().numpy(), np.float32)
+            for i, g in enumerate(grads)]
+    want = go.FedAvgOracle({}).aggregate(go.build_dense_G(rows, np.float32))
+    Cs = [Compression(cfg) for _ in range(3)]
+    agg = Aggregator({"aggregation_scheme": "fed_avg", "device_budget_bytes": _budget(N, 2)})
+    agg.aggregate_grads([_Client(i, g, Cs[i % 3]) for i, g in enumerate(grads)])
+    assert agg.agg_path == "stream"
+    assert agg.agg_grad.tobytes() == want.tobytes()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["full", "dropout-unbiased", "rand"])
+def test_aggregator_streams_over_a_device_ring(name):
+    """aggregation_config["devices"] = [0, 0, 0]: three pipelines (stand-ins for three GPUs),
+    one host thread each, the groups dealt round-robin and the masks still drawn in row
+    order: byte-equal, RNG state equal."""
+    pytest.importorskip("torch")
+    from openmsftl_amd import Compression
+    from openmsftl_amd.aggregation import Aggregator
+    from openmsftl_amd.pipeline import DeviceRing
+    grads = _grads(M, N, seed=3)
+    seed = 8
+    want, nxt = _reference_round([CFGS[name]] * M, grads, seed)
+    agg = Aggregator({"aggregation_scheme": "fed_avg", "devices": [0, 0, 0],
+                      "device_budget_bytes": _budget(N, 2, sets=2)})
+    for _ in range(2):                                      # reused pipelines
+        np.random.seed(seed)
+        agg.aggregate_grads([_Client(i, g, Compression(CFGS[name])) for i, g in enumerate(grads)])
+        assert int(np.random.randint(0, 2 ** 31 - 1)) == nxt
+        (pipe,) = agg._host_pipelines.values()
+        assert isinstance(pipe, DeviceRing) and pipe.group == 2
+        assert agg.agg_grad.tobytes() == want.tobytes()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["dropout-biased", "dropout-unbiased", "rand", "full"])
+def test_aggregator_streams_nonfinite_gradients(name):
+    """Gradients holding +-inf and NaN: a dropped inf/NaN is g * 0 = NaN in the reference's
+    float64 row (compression.py:52, :59), kept ones pass through; NaN where the reference has
+    NaN, the other bytes equal."""
+    pytest.importorskip("torch")
+    from openmsftl_amd import Compression
+    from openmsftl_amd.aggregation import Aggregator
+    grads = _grads(6, N, seed=99)
+    for j, g in enumerate(grads):
+        g[j::997] = np.inf
+        g[j + 3::1999] = -np.inf
+        g[j + 5::4001] = np.nan
+    seed = 17
+    with np.errstate(invalid="ignore", over="ignore"):
+        want, nxt = _reference_round([CFGS[name]] * 6, grads, seed)
+    agg = Aggregator({"aggregation_scheme": "fed_avg", "device_budget_bytes": _budget(N, 2)})
+    np.random.seed(seed)
+    agg.aggregate_grads([_Client(i, g, Compression(CFGS[name])) for i, g in enumerate(grads)])
+    assert int(np.random.randint(0, 2 ** 31 - 1)) == nxt
+    got = agg.agg_grad
+    nan = np.isnan(want)
+    assert nan.any()
+    np.testing.assert_array_equal(np.isnan(got), nan)
+    assert got[~nan].tobytes() == want[~nan].tobytes()
+
+
+@pytest.mark.gpu
+def test_aggregator_stream_draw_error_is_the_references():
+    """A client whose dropout_p makes np.random.binomial raise: the streamed round raises the
+    same ValueError (the generic path and the reference raise it at that row)."""
+    pytest.importorskip("torch")
+    from openmsftl_amd.aggregation import Aggregator
+    grads = _grads(4, N, seed=1)
+    cfgs = [CFGS["dropout-biased"]] * 2 + [{"compression_function": "dropout-biased",
+                                            "dropout_p": -0.5}] * 2
+    agg = Aggregator({"aggregation_scheme": "fed_avg"})
+    with pytest.raises(ValueError):
+        agg.aggregate_grads([_Client(i, g, _RefCompression(c))
+                             for i, (g, c) in enumerate(zip(grads, cfgs))])
