@@ -25,13 +25,14 @@
  * thread-local).  Device-side outcomes (e.g. the sampled bracket missing) are reported in the
  * packet header's `status`, read by the host after the stream is synchronised.
  *
- * One encode at a time per device: the encode kernels (fc_topk_encode*, fc_topk_encode_batch*,
- * fc_mask_encode, fc_topk_dense_f64*) hold a client's workgroups in bounded in-kernel waits that
- * assume no OTHER such kernel is dispatched beside them; two of them on two streams of one
- * device can stall each other to the bound (the clients then report FC_STATUS_TIMEOUT /
- * FC_STATUS_RETRY_EXACT: correct after the exact re-encode, but ~40 ms late).  Queue encodes on
- * one stream, or order them with events (the Python layer does: codec._ordered_encode).
- * Decodes, folds and sums have no such waits and may run beside anything.
+ * Concurrency: every entry point may run beside any other kernel, on any stream, with one
+ * exception.  fc_topk_encode (key_mode MAGNITUDE, 0 < k < n) and fc_topk_encode_dense launch
+ * k_fused_mag, whose compaction workgroups wait in-kernel (bounded) for the bracket its sample
+ * workgroups publish; two such launches on two streams of one device can stall each other to
+ * the bound (the call then reports FC_STATUS_RETRY_EXACT: correct after the exact re-encode,
+ * but late).  Queue those two on one stream, or order them with events (the Python layer
+ * does: codec._fused_encode).  The batched, mask, rand-k, float64, exact, decode and fold
+ * kernels synchronise only through last-arriver tickets (no workgroup waits for another).
  */
 #ifndef FEDCODEC_H_
 #define FEDCODEC_H_

@@ -177,7 +177,8 @@ def encode_top(g: torch.Tensor, k: int, *, key_mode: int = L.FC_KEY_MAGNITUDE, s
         packet = Packet.alloc(n, L.FC_FMT_IDXVAL, g.device, k=k)
     packet.k = k
     fn = lib.fc_topk_encode_exact if exact else lib.fc_topk_encode
-    with _ordered_encode(g.device):
+    fused = not exact and key_mode == L.FC_KEY_MAGNITUDE and 0 < k < n
+    with (_fused_encode(g.device) if fused else contextlib.nullcontext()):
         L.check(fn(_vp(g), n, k, key_mode, seed, offset, _vp(packet.idx), _vp(packet.val),
                    packet.capacity, _vp(packet.cnt), _vp(packet.qoff), _vp(packet.hdr), _vp(ws.buf),
                    ws.nbytes, _stream(g.device)), "fc_topk_encode")
@@ -211,7 +212,7 @@ def compress_top_dense(g: torch.Tensor, k: int, out: Optional[torch.Tensor] = No
     lib = L.load()
     ws = Workspace.get(n, g.device)
     packet.k = k
-    with _ordered_encode(g.device):
+    with _fused_encode(g.device):
         L.check(lib.fc_topk_encode_dense(_vp(g), n, k, _vp(packet.idx), _vp(packet.val),
                                          packet.capacity, _vp(packet.cnt), _vp(packet.qoff),
                                          _vp(packet.hdr), _vp(ws.buf), ws.nbytes, _vp(out),
@@ -252,39 +253,33 @@ class BatchWorkspace:
 
 _SIDE: dict = {}
 _MAX_SIDE = 4          # GPU_MAX_HW_QUEUES is 4: more forked streams would share queues
-# Above 2^27 elements per client a batched k_resolve gives each client more than
-# kResolveGridBatch (16) workgroups, up to 512, which wait for each other in-kernel: such
-# batches run on one stream, where at most one client is ever partly dispatched
-# (fc_topk.hip, k_resolve's residency note).  Packets are identical either way.
-_ONE_STREAM_N = 1 << 27
-# Encodes on one device never run concurrently.  k_fused_mag, k_sample1 and k_resolve hold a
-# client's workgroups in in-kernel waits, and two such launches on two queues are dispatched to
-# the 8 XCDs interleaved, so each XCD can fill up with waiters whose partners are queued on
-# another full XCD.  Measured on the GPU box: configs[2] with two sub-batches on two streams
-# stalled both k_resolve launches to the spin bound (42 ms, the clients then RETRY) in about 1
-# step in 70 (tools/stall_probe.py).  Lone encodes of one length also share one Workspace.
-# Every encode launch is therefore ordered after the device's previous one: when it is queued
-# on another stream than that one, it waits for an event recorded there (nothing is recorded
-# while the encodes stay on one stream).  One launch alone dispatches its clients in order and
-# always drains.
-_LAST_ENC: dict = {}                    # device index -> stream of the last encode queued there
-_ENC_LOCK = threading.RLock()
+# One kernel holds workgroups in an in-kernel wait: k_fused_mag, the lone magnitude encode
+# (fc_topk_encode, fc_topk_encode_dense), whose compaction workgroups poll for the bracket its
+# sample workgroups publish.  Two such launches on two queues are dispatched to the 8 XCDs
+# interleaved, so an XCD can fill up with waiters whose partners are queued on another full
+# XCD (round 4 measured this stall, to the spin bound, with the then-waiting k_resolve).  Every
+# fused encode on a device is therefore queued after the device's previous one when that one
+# went to another stream: an event recorded right after each fused encode (so a later encode
+# waits for that encode only, not for work queued behind it).  Every other encode kernel —
+# batched, mask, rand-k, fp64, exact — has only last-arriver tickets and runs beside anything.
+_FUSED_LAST: dict = {}                  # device index -> (stream, event after its last fused encode)
+_FUSED_LOCK = threading.RLock()
 
 
 @contextlib.contextmanager
-def _ordered_encode(dev: torch.device):
-    """Queue the encode launched inside this block on the current stream after the device's
-    previous encode (held under a lock, so another host thread cannot slip in between)."""
+def _fused_encode(dev: torch.device):
+    """Queue the fused encode launched inside this block after the device's previous fused
+    encode (held under a lock, so another host thread cannot slip in between)."""
     key = dev.index if dev.index is not None else torch.cuda.current_device()
     stream = torch.cuda.current_stream(dev)
-    with _ENC_LOCK:
-        last = _LAST_ENC.get(key)
-        if last is not None and last != stream:
-            ev = torch.cuda.Event()
-            ev.record(last)
-            stream.wait_event(ev)
+    with _FUSED_LOCK:
+        last = _FUSED_LAST.get(key)
+        if last is not None and last[0] != stream:
+            stream.wait_event(last[1])
         yield
-        _LAST_ENC[key] = stream
+        ev = last[1] if last is not None else torch.cuda.Event()
+        ev.record(stream)
+        _FUSED_LAST[key] = (stream, ev)
 
 
 def _side_streams(dev: torch.device, count: int = 2) -> list:
@@ -321,8 +316,8 @@ def encode_top_batch(grads: Sequence[torch.Tensor], k: int, *,
     """Top-k (or native rand-k) of M equal-length gradients in ONE launch per pipeline stage
     (fc_topk_encode_batch).  Same packets, bit for bit, as M calls of :func:`encode_top`.
     ``jobs``: a prebuilt :func:`encode_jobs` array for these exact grads/packets.
-    ``streams``: sub-batches launched on that many forked streams (joined before return), one
-    after the other (batched encodes on a device never overlap: see ``_LAST_ENC``);
+    ``streams``: sub-batches launched on that many forked streams (joined before return),
+    free to run concurrently (the batched kernels never wait in-kernel);
     ``groups``: sub-batch sizes (default: ``streams`` equal parts), dealt to the streams in turn.
     Pipelining (bench.py): ``part`` = FC_PART_SAMPLE or FC_PART_FINISH runs one half of the
     pipeline (fc_topk_encode_batch_part; the same ``groups`` / ``streams`` for both halves, so
@@ -377,8 +372,6 @@ def encode_top_batch(grads: Sequence[torch.Tensor], k: int, *,
         jobs._fc_grefs = [weakref.ref(g) for g in grads]
         jobs._fc_prefs = [weakref.ref(p) for p in packets]
     nside = max(1, min(int(streams), m, _MAX_SIDE))
-    if n > _ONE_STREAM_N:
-        nside = 1
     if groups is None:
         groups = [(i + 1) * m // nside - i * m // nside for i in range(nside)]
     groups = [int(x) for x in groups]
@@ -386,15 +379,13 @@ def encode_top_batch(grads: Sequence[torch.Tensor], k: int, *,
         raise ValueError(f"groups {groups} must be positive sizes summing to {m} clients")
     if nside == 1 or len(groups) == 1:
         ws = BatchWorkspace.get(n, m, dev)
-        with _ordered_encode(dev):
-            L.check(lib.fc_topk_encode_batch_part(_vp(jobs), m, n, k, key_mode, packets[0].capacity,
-                                                  _vp(ws.buf), ws.nbytes, part, _stream(dev)),
-                    "fc_topk_encode_batch")
+        L.check(lib.fc_topk_encode_batch_part(_vp(jobs), m, n, k, key_mode, packets[0].capacity,
+                                              _vp(ws.buf), ws.nbytes, part, _stream(dev)),
+                "fc_topk_encode_batch")
     else:
-        # Sub-batches on forked streams (group i on stream i % streams), launched one after
-        # the other (``_LAST_ENC``: two concurrent batched encodes can stall each other to the
-        # spin bound).  Packets are identical; the caller's stream joins every fork before
-        # this returns, so later work (and frees) stay ordered.
+        # Sub-batches on forked streams (group i on stream i % streams), free to overlap.
+        # Packets are identical; the caller's stream joins every fork before this returns, so
+        # later work (and frees) stay ordered.
         main = torch.cuda.current_stream(dev)
         job_bytes = ctypes.sizeof(L.EncodeJob)
         base = jobs.data_ptr()
@@ -407,7 +398,7 @@ def encode_top_batch(grads: Sequence[torch.Tensor], k: int, *,
         lo = 0
         for i, size in enumerate(groups):
             side = sides[i % nside]
-            with torch.cuda.stream(side), _ordered_encode(dev):
+            with torch.cuda.stream(side):
                 ws = BatchWorkspace.get(n, size, dev, slot=i)
                 L.check(lib.fc_topk_encode_batch_part(ctypes.c_void_p(base + lo * job_bytes),
                                                       size, n, k, key_mode, packets[0].capacity,
@@ -430,8 +421,7 @@ def encode_fold_batch(grads: Sequence[torch.Tensor], k: int, weights, out: torch
     sub-batch i is encoded on forked stream i and folded there as soon as it is encoded,
     continuing sub-batch i-1's partial sum (an event orders the folds, so the rows are added
     in G's order: bit-identical to :func:`encode_top_batch` + :func:`decode_accumulate`), while
-    sub-batch i+1 encodes on its own stream (the encodes themselves run one after the other,
-    ``_LAST_ENC``).  ``out`` holds the aggregate once the
+    sub-batch i+1 encodes on its own stream.  ``out`` holds the aggregate once the
     caller's stream (joined at return) reaches it.  Returns an event recorded once every
     sub-batch is ENCODED (the folds may still run); ``status=(src, dst)``: ``dst.copy_(src)``
     (e.g. the packet headers' status words into pinned host memory) is queued right then, so
@@ -452,8 +442,6 @@ def encode_fold_batch(grads: Sequence[torch.Tensor], k: int, weights, out: torch
     if views is None:
         views = views_tensor(packets, weights, dev)
     nside = max(1, min(int(streams), m, _MAX_SIDE))
-    if n > _ONE_STREAM_N:
-        nside = 1                                   # (k_resolve residency, see encode_top_batch)
     groups = [(i + 1) * m // nside - i * m // nside for i in range(nside)]
     jb, vb = ctypes.sizeof(L.EncodeJob), ctypes.sizeof(L.PacketView)
     main = torch.cuda.current_stream(dev)
@@ -469,11 +457,10 @@ def encode_fold_batch(grads: Sequence[torch.Tensor], k: int, weights, out: torch
         with torch.cuda.stream(side):
             side.wait_event(start)
             ws = BatchWorkspace.get(n, size, dev, slot=i)
-            with _ordered_encode(dev):
-                L.check(lib.fc_topk_encode_batch(ctypes.c_void_p(jobs.data_ptr() + lo * jb), size, n,
-                                                 k, L.FC_KEY_MAGNITUDE, packets[0].capacity,
-                                                 _vp(ws.buf), ws.nbytes, _stream(dev)),
-                        "fc_topk_encode_batch")
+            L.check(lib.fc_topk_encode_batch(ctypes.c_void_p(jobs.data_ptr() + lo * jb), size, n,
+                                             k, L.FC_KEY_MAGNITUDE, packets[0].capacity,
+                                             _vp(ws.buf), ws.nbytes, _stream(dev)),
+                    "fc_topk_encode_batch")
             for p, g in zip(packets[lo:hi], grads[lo:hi]):
                 p.k = k
                 p._enc = (g, k, L.FC_KEY_MAGNITUDE, 0, 0)
@@ -513,11 +500,10 @@ def resolve(packets: Sequence[Packet]) -> int:
             raise L.FedCodecError(f"packet status {h.status}")
         g, k, key_mode, seed, offset = p._enc
         ws = Workspace.get(g.numel(), g.device)
-        with _ordered_encode(g.device):
-            L.check(lib.fc_topk_encode_exact(_vp(g), g.numel(), k, key_mode, seed, offset,
-                                             _vp(p.idx), _vp(p.val), p.capacity, _vp(p.cnt),
-                                             _vp(p.qoff), _vp(p.hdr), _vp(ws.buf), ws.nbytes,
-                                             _stream(g.device)), "fc_topk_encode_exact")
+        L.check(lib.fc_topk_encode_exact(_vp(g), g.numel(), k, key_mode, seed, offset,
+                                         _vp(p.idx), _vp(p.val), p.capacity, _vp(p.cnt),
+                                         _vp(p.qoff), _vp(p.hdr), _vp(ws.buf), ws.nbytes,
+                                         _stream(g.device)), "fc_topk_encode_exact")
         redo += 1
         p._dense_only = False                        # a full packet now
         h2 = p.header()
@@ -541,12 +527,11 @@ def encode_mask(g: torch.Tensor, codec: int, *, p: float = 0.5,
         raise ValueError("mask_bits must be an int32 CUDA tensor of ceil(n/32) words")
     if packet is None:
         packet = Packet.alloc(n, fmt, g.device)
-    with _ordered_encode(g.device):
-        L.check(lib.fc_mask_encode(_vp(g), n, codec, _vp(mask_bits), float(p), seed, offset, fmt,
-                                   _vp(packet.idx), _vp(packet.val), _vp(packet.bitmap),
-                                   packet.capacity, _vp(packet.cnt), _vp(packet.qoff),
-                                   _vp(packet.hdr), _vp(ws.buf), ws.nbytes, _stream(g.device)),
-                "fc_mask_encode")
+    L.check(lib.fc_mask_encode(_vp(g), n, codec, _vp(mask_bits), float(p), seed, offset, fmt,
+                               _vp(packet.idx), _vp(packet.val), _vp(packet.bitmap),
+                               packet.capacity, _vp(packet.cnt), _vp(packet.qoff),
+                               _vp(packet.hdr), _vp(ws.buf), ws.nbytes, _stream(g.device)),
+            "fc_mask_encode")
     return packet
 
 
@@ -656,15 +641,13 @@ def div_scalar(x: torch.Tensor, d: float) -> torch.Tensor:
 
 
 # ---- float64 gradients (attack_models.py:105-106 -> aggregation.py:61) ----------------------
-_F64_STATUS: dict = {}
-
-
-def _f64_status(device: torch.device) -> torch.Tensor:
-    key = (device.index if device.index is not None else torch.cuda.current_device(),
-           torch.cuda.current_stream(device).cuda_stream)
-    st = _F64_STATUS.get(key)
-    if st is None:
-        st = _F64_STATUS[key] = torch.zeros(1, dtype=_U32, device=device)
+def _f64_status(out: torch.Tensor) -> torch.Tensor:
+    """The device status word of ONE output (k_compact64 sets it OK, k_resolve64 raises it to
+    RETRY): each output keeps its own, so several unchecked encodes are each resolvable."""
+    st = getattr(out, "_fc_f64_status", None)
+    if st is None or st.device != out.device:
+        st = torch.empty(1, dtype=_U32, device=out.device)
+        out._fc_f64_status = st
     return st
 
 
@@ -676,7 +659,7 @@ def compress_top_dense_f64(g: torch.Tensor, k: int, *, key_mode: int = L.FC_KEY_
     dense float64 q (same tie rule as fp32).  'top' with 0 < k < n takes the sampled path
     (fc_topk_dense_f64_sampled: one streaming pass); ``check=True`` reads its status (one
     sync) and re-runs a missed bracket exactly; with ``check=False`` call
-    :func:`resolve_f64` after the last call on this stream.  Native rand-k, trivial k and
+    :func:`resolve_f64` on the output later (each output has its own status word).  Native rand-k, trivial k and
     ``exact=True``: the exact radix select (fc_topk_dense_f64)."""
     _require_cuda_f32(g, align=8, dtype=torch.float64)
     n = g.numel()
@@ -692,25 +675,25 @@ def compress_top_dense_f64(g: torch.Tensor, k: int, *, key_mode: int = L.FC_KEY_
     sampled = (not exact and key_mode == L.FC_KEY_MAGNITUDE and 0 < k < n
                and g.data_ptr() % 16 == 0 and out.data_ptr() % 16 == 0)
     if sampled:
-        st = _f64_status(g.device)
-        with _ordered_encode(g.device):
-            L.check(lib.fc_topk_dense_f64_sampled(_vp(g), n, k, _vp(out), _vp(ws.buf), ws.nbytes,
-                                                  _vp(st), _stream(g.device)),
-                    "fc_topk_dense_f64_sampled")
+        st = _f64_status(out)
+        L.check(lib.fc_topk_dense_f64_sampled(_vp(g), n, k, _vp(out), _vp(ws.buf), ws.nbytes,
+                                              _vp(st), _stream(g.device)),
+                "fc_topk_dense_f64_sampled")
         out._fc_f64_enc = (g, k)
         if check:
             resolve_f64(out)
         return out
-    with _ordered_encode(g.device):
-        L.check(lib.fc_topk_dense_f64(_vp(g), n, k, key_mode, seed, offset, _vp(out), _vp(ws.buf),
-                                      ws.nbytes, _stream(g.device)), "fc_topk_dense_f64")
+    L.check(lib.fc_topk_dense_f64(_vp(g), n, k, key_mode, seed, offset, _vp(out), _vp(ws.buf),
+                                  ws.nbytes, _stream(g.device)), "fc_topk_dense_f64")
     return out
 
 
 def resolve_f64(out: torch.Tensor) -> int:
-    """After sampled fp64 encodes on the current stream: if the LAST one's bracket missed
-    (its status word), redo it exactly into ``out``.  Returns 1 if it did, else 0."""
-    st = _f64_status(out.device)
+    """After a sampled fp64 encode into ``out`` (check=False): if its bracket missed (the
+    output's own status word), redo it exactly into ``out``.  Returns 1 if it did, else 0."""
+    st = getattr(out, "_fc_f64_status", None)
+    if st is None or getattr(out, "_fc_f64_enc", None) is None:
+        return 0                                   # not a sampled encode's output
     if int(st.item()) == L.FC_STATUS_OK:
         return 0
     g, k = out._fc_f64_enc

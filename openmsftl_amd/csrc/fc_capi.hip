@@ -307,13 +307,24 @@ static uint32_t resolve_grid(uint32_t nchunks, uint32_t want) {
 #ifndef FC_RESOLVE_CPW
 #define FC_RESOLVE_CPW 8          // lone encode: >= this many chunks per k_resolve workgroup
 #endif
-static int launch_resolve(const ResolveArgs& a, hipStream_t s) {
+// k_resolve<true> (a.rbin: the compaction left the binning to the resolve) then k_resolve<false>:
+// no workgroup of either launch waits for another (only last-arriver tickets), so they are
+// safe beside any other kernel, encodes on other streams included
+static int launch_resolve(const ResolveArgs& a, hipStream_t s, dim3 grid) {
   TimedLaunch t(FC_TIME_ENGINE, s);
+  if (a.rbin) {
+    hipLaunchKernelGGL(k_resolve<true>, grid, dim3(kBlock), 0, s, a);
+    FC_LAUNCHED("k_resolve<bin>");
+  }
+  hipLaunchKernelGGL(k_resolve<false>, grid, dim3(kBlock), 0, s, a);
+  FC_LAUNCHED("k_resolve<gather>");
+  return FC_OK;
+}
+
+static int launch_resolve(const ResolveArgs& a, hipStream_t s) {
   const uint32_t want = std::max<uint32_t>(32u, std::min<uint32_t>((uint32_t)kResolveGrid,
                                             (a.nchunks + FC_RESOLVE_CPW - 1) / FC_RESOLVE_CPW));
-  hipLaunchKernelGGL(k_resolve, dim3(resolve_grid(a.nchunks, want)), dim3(kBlock), 0, s, a);
-  FC_LAUNCHED("k_resolve");
-  return FC_OK;
+  return launch_resolve(a, s, dim3(resolve_grid(a.nchunks, want)));
 }
 
 extern "C" {
@@ -429,7 +440,7 @@ int fc_topk_encode(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_
   if (key_mode == FC_KEY_MAGNITUDE && fused_enabled()) {
     rc = launch_fused(ca, P, hi, sgrid, s);
     if (rc) return rc;
-    ra.rbin = FC_FUSED_BIN_PKT ? 0u : 1u;
+    ra.rbin = 0;                     // k_fused_mag binned the candidates
     return launch_resolve(ra, s);
   }
   if (key_mode == FC_KEY_PHILOX)      // uniform keys: the analytical bracket, no sample
@@ -454,7 +465,7 @@ int fc_topk_encode_dense(const float* g, uint64_t n, uint64_t k, uint16_t* idx, 
                      ws_bytes, &ca, &ea, &ra, &hi);
   if (rc) return rc;
   ca.dense = dense;
-  if (fused_enabled() && !FC_DENSE_PKT) {   // q is the product: the header says no entries
+  if (fused_enabled()) {             // q is the product: the header says no entries
     hi.format = FC_FMT_DENSE;
     ca.HI.format = FC_FMT_DENSE;
   }
@@ -464,7 +475,7 @@ int fc_topk_encode_dense(const float* g, uint64_t n, uint64_t k, uint16_t* idx, 
   if (fused_enabled()) {
     rc = launch_fused(ca, P, hi, sgrid, s);
     if (rc) return rc;
-    ra.rbin = FC_FUSED_BIN_DENSE ? 0u : 1u;
+    ra.rbin = 0;                     // k_fused_mag binned the candidates
   } else {
     ra.rbin = 1;
     rc = launch_sample(FC_KEY_MAGNITUDE, dim3(sgrid), g, P, 0ull, 0ull, ca.W, ca.ib, hdr, hi, nullptr, 0ull, s);
@@ -536,14 +547,8 @@ int fc_topk_encode_batch_part(const fc_encode_job* jobs, int m, uint64_t n, uint
     int rc = launch_compact_key(key_mode, ca, s, (uint32_t)m);
     if (rc) return rc;
   }
-  {
-    TimedLaunch t(FC_TIME_ENGINE, s);
-    // fewer resolve workgroups per client than a lone encode: the batch fills the chip
-    const uint32_t rg = resolve_grid(ca.nchunks, kResolveGridBatch);
-    hipLaunchKernelGGL(k_resolve, dim3(rg, (uint32_t)m), dim3(kBlock), 0, s, ra);
-    FC_LAUNCHED("k_resolve(batch)");
-  }
-  return FC_OK;
+  // fewer resolve workgroups per client than a lone encode: the batch fills the chip
+  return launch_resolve(ra, s, dim3(resolve_grid(ca.nchunks, kResolveGridBatch), (uint32_t)m));
 }
 
 int fc_mask_encode(const float* g, uint64_t n, int codec, const uint32_t* mask_bits, double p,
@@ -599,9 +604,6 @@ int fc_mask_encode(const float* g, uint64_t n, int codec, const uint32_t* mask_b
   return FC_OK;
 }
 
-#ifndef FC_DEC_Q
-#define FC_DEC_Q 1
-#endif
 int fc_decode_dense(const fc_packet_view* pkt, int format, uint64_t n, void* out, int out_f64,
                     fc_stream_t stream) {
   FC_CHECK(pkt && out, "NULL argument");
@@ -624,7 +626,7 @@ int fc_decode_dense(const fc_packet_view* pkt, int format, uint64_t n, void* out
     // dense decode: the quarter-owned waves of the fold (no barrier per chunk): 87.5 us at
     // 128 M against 109.5 for k_decode_sparse<false> and its per-chunk workgroup barriers
     // (at 16 M the barrier form is 0.5 us faster: 2048 one-chunk workgroups in ~2 rounds)
-    else if (FC_DEC_Q && num_chunks(n) >= 4096u)
+    else if (num_chunks(n) >= 4096u)
       hipLaunchKernelGGL((k_fold_q<false, true>), dim3(num_chunks(n)), dim3(kQBlock), 0, s, a);
     else hipLaunchKernelGGL(k_decode_sparse<false>, dim3(decode_grid(n, 4)), dim3(kSBlock), 0, s, a);
   } else {

@@ -128,18 +128,11 @@ __device__ __forceinline__ uint32_t lane63(uint32_t x) {
 }
 
 // float4 load of elements [e, e+4) with zero fill past n (16-B aligned base required)
-#ifndef FC_NT_LOADS
-#define FC_NT_LOADS 1
-#endif
 __device__ __forceinline__ float4 load4(const float* __restrict__ g, uint64_t e, uint64_t n) {
   if (e + 4 <= n) {
-#if FC_NT_LOADS
     typedef float f4v __attribute__((ext_vector_type(4)));
     const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(g + e));
     return make_float4(v.x, v.y, v.z, v.w);
-#else
-    return *reinterpret_cast<const float4*>(g + e);
-#endif
   }
   float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
   if (e + 0 < n) r.x = g[e + 0];
@@ -169,11 +162,7 @@ typedef uint32_t fc_u32x8 __attribute__((ext_vector_type(8)));
 typedef float fc_f4v __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) const fc_f4v fc_gf4v;
 __device__ __forceinline__ float4 load4_full(const float* p) {
-#if FC_NT_LOADS
   const fc_f4v v = __builtin_nontemporal_load((fc_gf4v*)p);
-#else
-  const fc_f4v v = *(fc_gf4v*)p;
-#endif
   return make_float4(v.x, v.y, v.z, v.w);
 }
 __device__ __forceinline__ float f4get(const float4& v, int j) {

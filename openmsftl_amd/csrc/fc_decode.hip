@@ -61,19 +61,12 @@ __device__ __forceinline__ bool entry_kept(const PktCache& c, uint32_t id, float
 
 // Dense fp32 results leave with non-temporal 16-B stores (written once, read by the next
 // kernel or D2H; the fused dense encode measured NT at 192 us against 269 for plain / sc1)
-#ifndef FC_DEC_NT
-#define FC_DEC_NT 1
-#endif
 template <typename OutT>
 __device__ __forceinline__ void store_out(OutT* out, uint64_t e, uint64_t n, const float4& v) {
   if (e + 4 <= n) {
     if constexpr (sizeof(OutT) == 4) {
-#if FC_DEC_NT
       typedef float f4v __attribute__((ext_vector_type(4)));
       __builtin_nontemporal_store(f4v{v.x, v.y, v.z, v.w}, reinterpret_cast<f4v*>(out + e));
-#else
-      *reinterpret_cast<float4*>(out + e) = v;
-#endif
       return;
     }
   }

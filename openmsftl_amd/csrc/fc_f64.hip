@@ -303,14 +303,13 @@ __global__ __launch_bounds__(kBlock) void k_div_scalar64(double* x, uint64_t n, 
 //                 beta holding it (the histogram, from L2) and gathers its chunks' candidates
 //                 in beta (a chunk whose candidates overflowed its slot is rescanned from
 //                 g); the last arriver sorts them (<= 2048, LDS) and picks T, the exact k-th
-//                 largest comp; a bracket that missed or a bin beta above 2048 -> RETRY
-//                 and publishes it (generation word); every workgroup then sets q[idx] = +0
-//                 for its candidates with comp < T (the grid, <= 256 workgroups, is
-//                 co-resident; the wait is bounded)
+//                 largest comp; a bracket that missed or a bin beta above 2048 -> RETRY.
+//                 q[idx] = +0 for the slack: every workgroup zeroes its candidates binned
+//                 below beta (below T whatever T is) in the gather pass, the last arriver the
+//                 entries of bin beta below T.  No workgroup waits for another.
 // The exact radix engine (<= 8 passes of 8N) stays the fallback and serves native rand-k.
 // --------------------------------------------------------------------------------------
 constexpr int kC64Slot = 128;                  // candidate comps per chunk (the 2 KB slot)
-constexpr uint32_t kSpinMax64 = 1u << 18;      // bounded waits (~60 ms): one that ends is a bug
 constexpr uint32_t kResolve64Grid = 256;       // k_resolve64 workgroups at most (co-resident)
 constexpr uint64_t kHdr64Off = 896;            // the sample's scratch packet header
 static_assert(kEng64Off + sizeof(Eng64State) <= kHdr64Off && kHdr64Off + sizeof(fc_packet_hdr) <= 1024,
@@ -324,7 +323,7 @@ __global__ __launch_bounds__(kBlock, 8) void k_sample64(const double* __restrict
                                                      HdrInit HI) {
   __shared__ SampleShared sm;
   sample_body<kKeyMag, false, double>(g, P, 0ull, 0ull, W, ib, hdr, HI, blockIdx.x, gridDim.x,
-                                      true, sm, 0u);
+                                      false, sm, 0u);   // every workgroup its own window: no wait
 }
 
 struct Fast64Args {
@@ -451,7 +450,6 @@ __global__ __launch_bounds__(kBlock) void k_resolve64(Fast64Args a) {
   const int tid = threadIdx.x;
   TopkState* S = a.S;
   const uint32_t c0 = blockIdx.x * a.per, c1 = min(c0 + a.per, a.nchunks);
-  const uint32_t gen0 = ld_agent(&a.E->gen);              // before the ticket: stable
   uint32_t se = 0, sc = 0;
   if (tid < kShards) { se = S->shard_ent[tid]; sc = S->shard_cnd[tid]; }
   uint32_t hv[kHistBins / kBlock];
@@ -477,10 +475,15 @@ __global__ __launch_bounds__(kBlock) void k_resolve64(Fast64Args a) {
   }
   __syncthreads();                                        // h (sv) is reused below
   if (!retry) {
+    // one pass: a candidate binned below beta is below T whatever T is (bins are in key order):
+    // zeroed at once; bin beta's candidates go to the small list for the last arriver
     for_cands64(a, c0, c1, t_lo, t_hi, [&](const u128& v) {
       const uint32_t key = (uint32_t)(v >> 64);           // = key64 >> 32: key32 before the clamp
       const uint32_t k32 = key > 0x7f800000u ? kNanKey : key;
-      if (((k32 - t_lo) >> sbin) == beta) {
+      const uint32_t b = (k32 - t_lo) >> sbin;
+      if (b < beta) {
+        a.out[(uint32_t)v] = 0.0;
+      } else if (b == beta) {
         const uint32_t q = atomicAdd(&s_cnt, 1u);
         if (q < (uint32_t)kSmallCap64) sv[q] = v;
       }
@@ -497,29 +500,13 @@ __global__ __launch_bounds__(kBlock) void k_resolve64(Fast64Args a) {
       }
     }
   }
-  auto fixup = [&](const u128& T) {
-    for_cands64(a, c0, c1, t_lo, t_hi, [&](const u128& v) {
-      if (v < T) a.out[(uint32_t)v] = 0.0;
-    });
-  };
-  if (!last_block_arrive_tree(a.tick, gridDim.x, blockIdx.x, &s_flag)) {
-    if (retry) return;                                    // (grid-uniform bracket miss)
-    if (tid == 0) {                                       // relaxed sc1 poll (bounded)
-      uint32_t it = 0;
-      while (ld_agent(&a.E->gen) == gen0 && ++it < kSpinMax64) __builtin_amdgcn_s_sleep(4);
-      s_flag = it < kSpinMax64 && ld_agent(&a.E->status) == (uint32_t)FC_STATUS_OK;
-      if (it >= kSpinMax64) atomicMax(a.status, (uint32_t)FC_STATUS_RETRY_EXACT);
-    }
-    __syncthreads();
-    if (!s_flag) return;
-    fixup(u128_of(ld_agent(&a.E->p_hi), ld_agent(&a.E->p_lo)));
-    return;
-  }
-  // ---- last workgroup: T = the r_in-th largest of bin beta, status, self-cleaning ----
+  // no workgroup waits for another: the last arriver finishes the call alone
+  if (!last_block_arrive_tree(a.tick, gridDim.x, blockIdx.x, &s_flag)) return;
+  // ---- last workgroup: T = the r_in-th largest of bin beta, the slack of bin beta, status,
+  // self-cleaning ----
   const bool err = ld_agent(&S->err) != 0u;
   const uint32_t got = ld_agent(&a.E->small_n);
   retry = retry || err || got != cnt_beta;
-  u128 T = 0;
   if (!retry) {
     uint32_t P2 = 1;
     while (P2 < cnt_beta) P2 <<= 1;
@@ -533,20 +520,16 @@ __global__ __launch_bounds__(kBlock) void k_resolve64(Fast64Args a) {
     }
     __syncthreads();
     bitonic_desc128(sv, P2);
-    T = sv[r_in - 1];
+    // T = sv[r_in - 1]: the entries after it are the slack of bin beta
+    for (uint32_t i = r_in + tid; i < cnt_beta; i += kBlock) a.out[(uint32_t)sv[i]] = 0.0;
   }
   for (int b = tid; b < kHistBins; b += kBlock) st_agent(&a.chist[b], 0u);
   if (tid == 0) {
     const uint32_t st = retry ? (uint32_t)FC_STATUS_RETRY_EXACT : (uint32_t)FC_STATUS_OK;
-    st_agent(&a.E->p_hi, (uint64_t)(T >> 64)); st_agent(&a.E->p_lo, (uint64_t)T);
-    st_agent(&a.E->status, st);
     a.E->small_n = 0;
     S->err = 0;
     atomicMax(a.status, st);                              // (k_compact64 reset it to OK)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    st_agent(&a.E->gen, gen0 + 1u);                       // T and status first
   }
-  if (!retry) fixup(T);
 }
 
 template __global__ void k_engine64<kKeyMag>(Engine64Args);

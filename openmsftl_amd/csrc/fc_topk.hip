@@ -265,11 +265,10 @@ __device__ __forceinline__ FineWin pilot_window(const T* __restrict__ g, const S
   return win_of(s_out[2], s_out[0]);
 }
 
-// One launch: grid (ceil(nseg / kSampleSegs), clients).  A lone client's launch (<= 256
-// workgroups, always co-resident) has workgroup 0 compute the window and publish it (sc1
-// payload + flag; the others load their segments meanwhile): 256 workgroups re-reading the same
-// 32 KB pilot took ~7 us of loads.  A batched launch (too many workgroups to wait on each
-// other) has every workgroup compute the window itself.
+// One launch: grid (ceil(nseg / kSampleSegs), clients).  k_sample1 has every workgroup compute
+// the window itself (no in-kernel wait); k_fused_mag's sample workgroups share workgroup 0's
+// (sc1 payload + flag; the others load their segments meanwhile): 256 workgroups re-reading the
+// same 32 KB pilot took ~7 us of loads.
 struct SampleShared {
   uint32_t h[kHistBins];                          // pilot histogram, then the sample's
   uint32_t s_tmp[8], s_out[4], s_flag, s_win[3];
@@ -430,7 +429,9 @@ __global__ __launch_bounds__(kBlock, 8) void k_sample1(const float* __restrict__
     HI.seed = seed; HI.offset = off;
     W = ws_shift(W, (uint64_t)blockIdx.y * ws_stride);
   }
-  sample_body<KM>(g, P, seed, off, W, ib, hdr, HI, blockIdx.x, gridDim.x, gridDim.y == 1, sm, 0u);
+  // every workgroup computes the pilot window itself (no workgroup of this launch waits for
+  // another: safe beside any other kernel); only k_fused_mag shares workgroup 0's window
+  sample_body<KM>(g, P, seed, off, W, ib, hdr, HI, blockIdx.x, gridDim.x, false, sm, 0u);
 }
 
 
@@ -846,9 +847,6 @@ __device__ __forceinline__ MagState mag_state(const TopkState* S) {
 // tools/shape_probe.hip) but are equal in the batched compaction and 15 % slower on the dense
 // path, whose 512 MB of q stores then compete with the gradient for the caches
 // (profiles/r02_ab_mag_load_kind.jsonl).
-#ifndef FC_MAG_NT_LOAD
-#define FC_MAG_NT_LOAD 1
-#endif
 template <int NW>
 __device__ __forceinline__ void mag_load(const float* g, uint32_t chunk, uint64_t n,
                                          float (&x)[MagGeo<NW>::kQ]) {
@@ -865,13 +863,7 @@ __device__ __forceinline__ void mag_load(const float* g, uint32_t chunk, uint64_
   }
   gf* gp = (gf*)g + base + l0;
 #pragma unroll
-  for (int q = 0; q < NQ; ++q) {
-#if FC_MAG_NT_LOAD
-    x[q] = __builtin_nontemporal_load(gp + (q >> 2) * IS + (q & 3) * 64);
-#else
-    x[q] = gp[(q >> 2) * IS + (q & 3) * 64];
-#endif
-  }
+  for (int q = 0; q < NQ; ++q) x[q] = __builtin_nontemporal_load(gp + (q >> 2) * IS + (q & 3) * 64);
 }
 
 // One workgroup per item (grid = (nchunks, clients)); <= 64 VGPRs, so 4 resident 512-thread
@@ -923,9 +915,6 @@ __device__ __forceinline__ void compact_mag_item(const CompactArgs& a0, const Ma
 #ifndef FC_MAG1_IL
 #define FC_MAG1_IL 64
 #endif
-#ifndef FC_MAG1_ROT
-#define FC_MAG1_ROT 0
-#endif
 // Dispatch order: workgroups are dispatched x-fastest, so the linear id L = y*nch + x is
 // re-mapped to interleave the chunks of FC_MAG1_IL clients (chunk-major within a group of
 // clients): FC_MAG1_IL address streams are in flight at once instead of one.  Measured
@@ -945,12 +934,6 @@ __device__ __forceinline__ void mag_item_of(uint32_t& client, uint32_t& chunk) {
   chunk = r / Ig;
   const uint32_t j = r - chunk * Ig;
   client = g * (uint32_t)FC_MAG1_IL + j;
-#if FC_MAG1_ROT
-  // client j of the group starts its walk j/Ig of the way through the gradient, so the
-  // concurrently read addresses of the group differ in their low bits too
-  chunk += (uint32_t)(((uint64_t)j * nch) / Ig);
-  if (chunk >= nch) chunk -= nch;
-#endif
 }
 
 template <int NW, bool DENSE = false, bool NTS = false>
@@ -986,29 +969,18 @@ __global__ __launch_bounds__(kCBlock, FC_MAG1_WAVES_PER_EU) void k_compact_mag1_
 // never waits on a chunk workgroup, so no wait can deadlock; a timed-out one (never expected)
 // sets S->err, and the resolve reports RETRY (the caller re-encodes exactly).
 // --------------------------------------------------------------------------------------
-#ifndef FC_FZ_SLEEP
-#define FC_FZ_SLEEP 4         // s_sleep argument of the chunk workgroups' bracket poll
-#endif
 union FusedShared {
   SampleShared s;
   MagShared m;
 };
 
 // Candidate binning inside the fused launch (one device-scope atomic per candidate into the
-// candidate histogram) or in k_resolve (rbin) — per variant, see fc_capi.hip.  Both lone paths
-// bin in-kernel since round 4: with the candidate histogram at its padded workspace offset
-// (fc_state.h) the atomics cost the 128 M packet encode +2 us in the fused kernel and save 8 us
-// of resolve (170 -> 165 us; 16 M: equal).  Round 3 had measured 197 vs 148 us — the
-// histogram's lines then collided in HBM with another hot line (profiles/r04_ab_fused_bin.jsonl).
-#ifndef FC_FUSED_BIN_DENSE
-#define FC_FUSED_BIN_DENSE 1
-#endif
-#ifndef FC_FUSED_BIN_PKT
-#define FC_FUSED_BIN_PKT 1
-#endif
-#ifndef FC_DENSE_PKT
-#define FC_DENSE_PKT 0        // 1: the dense path also writes every packet entry (A/B only)
-#endif
+// candidate histogram), so the resolve needs no binning launch.  Both lone paths bin in-kernel
+// since round 4: with the candidate histogram at its padded workspace offset (fc_state.h) the
+// atomics cost the 128 M packet encode +2 us in the fused kernel and save 8 us of resolve
+// (170 -> 165 us; 16 M: equal).  Round 3 had measured 197 vs 148 us — the histogram's lines
+// then collided in HBM with another hot line (profiles/r04_ab_fused_bin.jsonl).  The dense
+// path writes no packet entries (only an overflowed chunk's, which the resolve re-reads).
 template <bool DENSE, int NW>
 __device__ __forceinline__ void fused_mag_wg(const CompactArgs& a0, const SamplePlan& P,
                                              const HdrInit& HI, uint32_t nsamp) {
@@ -1029,7 +1001,7 @@ __device__ __forceinline__ void fused_mag_wg(const CompactArgs& a0, const Sample
   FC_TR(24);
   if (threadIdx.x == 0) {
     uint32_t it = 0;
-    while (ld_agent(&S->fz_pub) != pub && ++it < kSpinMax) __builtin_amdgcn_s_sleep(FC_FZ_SLEEP);
+    while (ld_agent(&S->fz_pub) != pub && ++it < kSpinMax) __builtin_amdgcn_s_sleep(4);
     if (it >= kSpinMax) st_agent(&S->err, 1u);
     MagState m;
     m.L64 = ld_agent(&S->L64);
@@ -1040,8 +1012,7 @@ __device__ __forceinline__ void fused_mag_wg(const CompactArgs& a0, const Sample
   __syncthreads();
   FC_TR(25);
   const MagState st = s_st;
-  constexpr bool kBin = DENSE ? FC_FUSED_BIN_DENSE != 0 : FC_FUSED_BIN_PKT != 0;
-  compact_mag_item<NW, MagShared, DENSE, kBin, !DENSE || FC_DENSE_PKT != 0>(a0, mag_out(a0, 0u), chunk, st, x, u.m);
+  compact_mag_item<NW, MagShared, DENSE, true, !DENSE>(a0, mag_out(a0, 0u), chunk, st, x, u.m);
   FC_TR(26);
 }
 template <bool DENSE>
@@ -1053,28 +1024,23 @@ template __global__ void k_fused_mag<false>(CompactArgs, SamplePlan, HdrInit, ui
 template __global__ void k_fused_mag<true>(CompactArgs, SamplePlan, HdrInit, uint32_t);
 
 // --------------------------------------------------------------------------------------
-// k_resolve: exact T64 from the bracket's candidates (fast path, one launch).
-//   totals from the sharded counters -> rank r = k - #(key > t_hi) -> every workgroup bins its
-//   chunks' candidates (candidate slot, or the entries slot when the chunk overflowed its
-//   candidate slot) into the 4096-bin candidate histogram -> grid barrier -> the bin beta
-//   holding rank r -> every workgroup gathers its candidates in beta -> the last workgroup
-//   sorts the <= 4096 survivors in LDS and picks T64.
-// fc_topk_encode_dense (a.dense set, one client): k_compact_mag1_dense wrote q = g at every
-// LISTED element (comp >= L64); the slack ones (comp < T64) must go back to +0.  Every slack
-// entry is a candidate of its chunk, so the workgroups that gathered a chunk range wait for the
-// last one to publish T64 (generation counter, release/acquire) and zero the slack of their
-// own range: no fix-up launch (it took 13.8 us per 128 M gradient as its own kernel).
-// The in-kernel waits (beta, "gathered", T64) need every workgroup of a client resident while
-// any of them spins.  A lone encode's grid is <= 512 workgroups (4 per CU by LDS: 1024 slots).
-// A batched launch dispatches its grid in order (x = the client's workgroups, fastest; dealt
-// round-robin to the 8 XCDs, in the same order on each), so at most its LAST client is partly
-// dispatched, and the complete clients before it free the slots it waits for.  Two batched
-// launches on concurrent queues are NOT safe: each XCD interleaves the two grids in its own
-// order, and can fill up with waiters whose partners sit queued behind another full XCD
-// (measured: two 64-client k_resolve launches, 16 workgroups per client, stalled to the spin
-// bound, 42 ms, in ~1 step in 70).  The host side (codec._LAST_ENC) never queues two batched
-// encodes on a device concurrently.  Every spin is bounded (FC_STATUS_TIMEOUT -> the exact
-// path).
+// k_resolve<BIN>: exact T64 from the bracket's candidates, in launches whose workgroups never
+// wait for each other (only last-arriver tickets):
+//   k_resolve<true>  (when the compaction did not bin the candidates: batched, unfused, rand-k)
+//     every workgroup bins its chunks' candidates (candidate slot, or the entries slot of a chunk
+//     whose candidates overflowed it) into the 4096-bin candidate histogram; the last arriver
+//     sums the shards, finds the bin beta holding rank r = k - #(key > t_hi) and stores it;
+//   k_resolve<false> every workgroup gathers its candidates in bin beta into the small list
+//     (beta from k_resolve<true>, or from the histogram k_fused_mag filled while it streamed);
+//     the last arriver sorts the <= 4096 survivors in LDS, picks T64 and writes the header.
+// fc_topk_encode_dense (a.dense, one client): the compaction wrote q = g at every LISTED
+// element (comp >= L64); the slack (comp < T64) must go back to +0.  Bins are in key order, so a
+// candidate binned below beta is below T64 whatever T64 is: every workgroup zeroes those of its
+// range before its ticket, and the last arriver zeroes the entries of bin beta below T64 from
+// the sorted list it holds (their comps carry the index).  No fix-up launch, no wait.
+// Round 4 had one launch whose workgroups waited in-kernel for the bin (and, dense, for T64):
+// safe only while every workgroup of a client was resident; two launches on two queues
+// interleaved by the XCDs stalled each other to the spin bound (42-84 ms, ~1 step in 70).
 // --------------------------------------------------------------------------------------
 struct ResolveArgs {
   uint32_t ib, nchunks;
@@ -1089,8 +1055,8 @@ struct ResolveArgs {
   const fc_encode_job* jobs;   // batched encode (see CompactArgs)
   uint64_t ws_stride;
   float* dense;                // fc_topk_encode_dense: zero the slack of q (one client)
-  uint32_t rbin;               // 1: bin the candidates here (the compaction did not: batched,
-                               // unfused and rand-k); 0: k_fused_mag filled the histogram
+  uint32_t rbin;               // 1: k_resolve<true> binned the candidates (the compaction did
+                               // not: batched, unfused and rand-k); 0: k_fused_mag did
 };
 
 // chunks per workgroup (their gather sizes live in LDS; the launches size the grid so that no
@@ -1098,21 +1064,20 @@ struct ResolveArgs {
 // 3 per CU) a 64-client batch's 1024 workgroups did not fit one round.
 constexpr int kResolveChunksMax = 1024;
 
+template <bool BIN>
 __global__ __launch_bounds__(kBlock) void k_resolve(ResolveArgs a0) {
   ResolveArgs a = a0;
   apply_job(a);
   __shared__ uint64_t sv[kSmallCap];                      // 32 KiB: histogram, then sort
   __shared__ uint32_t s_pre[kResolveChunksMax];           // per-chunk gather sizes
-  __shared__ uint32_t s_tmp[8], s_out[4], s_flag, s_cnt, s_base, s_tot[2], s_st;
+  __shared__ uint32_t s_tmp[8], s_out[4], s_flag, s_cnt, s_base, s_tot[2];
   __shared__ uint64_t s_T;
   uint32_t* h = reinterpret_cast<uint32_t*>(sv);          // 4096 bins = 16 KiB
   TopkState* S = a.W.st;
   const int tid = threadIdx.x;
   FC_TR(8);
-  const uint32_t gen0 = a.dense ? ld_agent(&S->gen) : 0u; // before the tickets: stable
-  const uint32_t hgen0 = ld_agent(&S->hgen);
   // ---- totals (sharded counters written by the compaction) and the bracket: one round of
-  // independent loads (they were three dependent rounds, ~9 us) ----
+  // independent loads ----
   uint32_t se = 0, sc = 0;
   if (tid < kShards) { se = S->shard_ent[tid]; sc = S->shard_cnd[tid]; }
   const uint32_t t_lo = S->t_lo, t_hi = S->t_hi, sbin = S->sbin, err = S->err;
@@ -1124,17 +1089,23 @@ __global__ __launch_bounds__(kBlock) void k_resolve(ResolveArgs a0) {
   const uint32_t c1 = min(c0 + per, a.nchunks);
   const uint32_t nc = c1 > c0 ? c1 - c0 : 0u;
   const uint32_t cc_early = (nc <= (uint32_t)kBlock && (uint32_t)tid < nc) ? a.W.ccnt[c0 + tid] : 0u;
+  // the gather's bin: the compaction's histogram (every workgroup reads it), or k_resolve<true>'s
   uint32_t hv[kHistBins / kBlock];
+  const bool own_hist = !BIN && !rbin;
 #pragma unroll
-  for (int j = 0; j < kHistBins / kBlock; ++j) hv[j] = rbin ? 0u : a.W.chist[j * kBlock + tid];
+  for (int j = 0; j < kHistBins / kBlock; ++j) hv[j] = own_hist ? a.W.chist[j * kBlock + tid] : 0u;
   static_assert(kShards == 64, "shard totals: one wave");
   if (tid < 64) {
     se = wave_sum(se);
     sc = wave_sum(sc);
-    if (tid == 0) { s_tot[0] = se; s_tot[1] = sc; s_st = 0; }
+    if (tid == 0) {
+      s_tot[0] = se; s_tot[1] = sc;
+      if (!BIN && rbin) { s_out[0] = ld_agent(&S->rb_beta); s_out[1] = ld_agent(&S->rb_rin);
+                          s_out[2] = ld_agent(&S->rb_cnt); }
+    }
   }
 #pragma unroll
-  for (int j = 0; j < kHistBins / kBlock; ++j) h[j * kBlock + tid] = hv[j];   // (rbin: zeros)
+  for (int j = 0; j < kHistBins / kBlock; ++j) h[j * kBlock + tid] = hv[j];
   __syncthreads();
   const uint32_t n_ent = s_tot[0], n_cand = s_tot[1];
   const uint32_t n_hi = n_ent - n_cand;                   // listed above the bracket
@@ -1142,13 +1113,19 @@ __global__ __launch_bounds__(kBlock) void k_resolve(ResolveArgs a0) {
   const uint32_t rank = bad ? 0u : (uint32_t)(a.k - n_hi);
   bool retry = bad || per > (uint32_t)kResolveChunksMax;  // grid-uniform (exact path)
   uint32_t beta = 0, r_in = 1, cnt_beta = 0;
-  if (!rbin && !retry && rank > 0) {                      // the compaction's histogram
-    find_rank_desc(h, rank, s_tmp, s_out);
-    beta = s_out[0]; r_in = s_out[1]; cnt_beta = h[beta];
+  if (!BIN && !retry && rank > 0) {
+    if (own_hist) {
+      find_rank_desc(h, rank, s_tmp, s_out);
+      beta = s_out[0]; r_in = s_out[1]; cnt_beta = h[beta];
+    } else {
+      beta = s_out[0]; r_in = s_out[1]; cnt_beta = s_out[2];
+    }
     retry = cnt_beta > (uint32_t)kSmallCap || cnt_beta < r_in;
     __syncthreads();
   }
-  const bool walk = !retry && (rank > 0 || a.dense);      // uniform
+  const bool binning = BIN && !retry && rank > 0;         // grid-uniform
+  const bool walk = BIN ? binning : (!retry && (rank > 0 || a.dense));
+  if (BIN && !binning) return;   // nothing to bin (the gather launch sees the same retry / rank)
   // ---- per-chunk gather sizes: the candidate slot, or (bit 31) the entries slot of a chunk
   // whose candidates overflowed their slot ----
   if (walk) {
@@ -1210,118 +1187,95 @@ __global__ __launch_bounds__(kBlock) void k_resolve(ResolveArgs a0) {
       }
     }
   };
-  // ---- the candidate histogram: every workgroup bins the candidates of its chunk range in
-  // LDS and flushes the non-empty bins into one of kCandShards (2) shards (one shared
-  // histogram: its queued same-address atomics cost the lone encode 3 us; 4 / 8 shards: the
-  // last arriver's extra shard loads cost more, fc_state.h); the last arriver (two-level ticket)
-  // sums the shards, finds the bin beta holding rank r and publishes it (generation word
-  // hgen).  (The compaction used to add every candidate into the histogram with a global
-  // atomic: 5.7 % of that pass at 128 M.)  The wait
-  // is safe: a client's <= 256 workgroups are dispatched together and never wait on a later
-  // client; the spin is bounded (sets err: the call reports RETRY). ----
-  const bool binning = rbin && !retry && rank > 0;       // grid-uniform
-  if (binning) {
+  auto bin_of = [&](uint64_t v) { return (((uint32_t)(v >> a.ib)) - t_lo) >> sbin; };
+  if constexpr (BIN) {
+    // ---- the candidate histogram: every workgroup bins the candidates of its chunk range in
+    // LDS and flushes the non-empty bins into one of kCandShards (2) shards (one shared
+    // histogram: its queued same-address atomics cost the lone encode 3 us; 4 / 8 shards: the
+    // last arriver's extra shard loads cost more, fc_state.h); the last arriver (two-level
+    // ticket) sums the shards, finds the bin beta holding rank r and stores it for the gather
+    // launch.  (The compaction used to add every candidate into the histogram with a global
+    // atomic: 5.7 % of that pass at 128 M.) ----
     for_cands(false, [&](const uint64_t (&v)[kGatherU]) {
 #pragma unroll
       for (int u = 0; u < kGatherU; ++u)
-        if (v[u] != ~0ull) atomicAdd(&h[(((uint32_t)(v[u] >> a.ib)) - t_lo) >> sbin], 1u);
+        if (v[u] != ~0ull) atomicAdd(&h[bin_of(v[u])], 1u);
     });
     __syncthreads();
     FC_TR(29);
     flush_hist(a.W.chist + (blockIdx.x % kCandShards) * kHistBins, h);   // this workgroup's shard
     FC_TR(27);
-    if (last_block_arrive_tree(a.W.tick + 2 * kTickWords, gridDim.x, blockIdx.x, &s_flag)) {
-      // the last arriver sums the shards (every load first, then the clearing stores: their
-      // next use is the next call's atomics, after this launch), finds beta and publishes it
-      constexpr int kPer = kHistBins / kBlock;
-      uint32_t t[kPer];
+    if (!last_block_arrive_tree(a.W.tick + 2 * kTickWords, gridDim.x, blockIdx.x, &s_flag)) return;
+    // the last arriver sums the shards (every load first, then the clearing stores: their next
+    // use is the next call's atomics, after this launch), finds beta and stores it
+    constexpr int kPer = kHistBins / kBlock;
+    uint32_t t[kPer];
 #pragma unroll
-      for (int j = 0; j < kPer; ++j) t[j] = 0;
+    for (int j = 0; j < kPer; ++j) t[j] = 0;
 #pragma unroll
-      for (int sh = 0; sh < kCandShards; ++sh)
+    for (int sh = 0; sh < kCandShards; ++sh)
 #pragma unroll
-        for (int j = 0; j < kPer; ++j) t[j] += ld_agent(&a.W.chist[sh * kHistBins + j * kBlock + tid]);
+      for (int j = 0; j < kPer; ++j) t[j] += ld_agent(&a.W.chist[sh * kHistBins + j * kBlock + tid]);
 #pragma unroll
-      for (int j = 0; j < kPer; ++j) h[j * kBlock + tid] = t[j];
-      __syncthreads();
-      find_rank_desc(h, rank, s_tmp, s_out);
-      if (tid == 0) {
-        st_agent(&S->rb_beta, s_out[0]); st_agent(&S->rb_rin, s_out[1]);
-        st_agent(&S->rb_cnt, h[s_out[0]]);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        st_agent(&S->hgen, hgen0 + 1u);
-      }
-      for (int i = tid; i < kHistBins * kCandShards / 4; i += kBlock)
-        reinterpret_cast<uint4*>(a.W.chist)[i] = make_uint4(0u, 0u, 0u, 0u);
-    } else if (tid == 0) {                                // relaxed sc1 poll (bounded)
-      uint32_t it = 0;
-      while (ld_agent(&S->hgen) == hgen0 && ++it < kSpinMax) __builtin_amdgcn_s_sleep(2);
-      if (it >= kSpinMax) { s_st = 1u; st_agent(&S->err, 1u); }
-    }
-    if (tid == 0 && s_st == 0) {
-      s_out[0] = ld_agent(&S->rb_beta); s_out[1] = ld_agent(&S->rb_rin); s_out[2] = ld_agent(&S->rb_cnt);
-    }
+    for (int j = 0; j < kPer; ++j) h[j * kBlock + tid] = t[j];
     __syncthreads();
+    find_rank_desc(h, rank, s_tmp, s_out);
+    if (tid == 0) {
+      st_agent(&S->rb_beta, s_out[0]); st_agent(&S->rb_rin, s_out[1]);
+      st_agent(&S->rb_cnt, h[s_out[0]]);
+    }
+    for (int i = tid; i < kHistBins * kCandShards / 4; i += kBlock)
+      reinterpret_cast<uint4*>(a.W.chist)[i] = make_uint4(0u, 0u, 0u, 0u);
     FC_TR(28);
-    if (s_st != 0) {
-      retry = true;                                       // (err makes the call RETRY)
-    } else {
-      beta = s_out[0]; r_in = s_out[1]; cnt_beta = s_out[2];
-      retry = cnt_beta > (uint32_t)kSmallCap || cnt_beta < r_in;
-    }
-    __syncthreads();
-  }
-  FC_TR(9);
-  if (!retry && rank > 0) {
-    // gather bin beta into the LDS list (sv reused after the histogram)
-    if (tid == 0) s_cnt = 0;
-    __syncthreads();
-    for_cands(rbin, [&](const uint64_t (&v)[kGatherU]) {
+    return;
+  } else {
+    // ---- gather bin beta into the LDS list, then into the small list ----
+    if (!retry && rank > 0) {
+      if (tid == 0) s_cnt = 0;
+      __syncthreads();
+      for_cands(false, [&](const uint64_t (&v)[kGatherU]) {
 #pragma unroll
-      for (int u = 0; u < kGatherU; ++u) {
-        if (v[u] != ~0ull && ((((uint32_t)(v[u] >> a.ib)) - t_lo) >> sbin) == beta) {
-          const uint32_t q = atomicAdd(&s_cnt, 1u);
-          if (q < (uint32_t)kSmallCap) sv[q] = v[u];
+        for (int u = 0; u < kGatherU; ++u) {
+          if (v[u] != ~0ull && bin_of(v[u]) == beta) {
+            const uint32_t q = atomicAdd(&s_cnt, 1u);
+            if (q < (uint32_t)kSmallCap) sv[q] = v[u];
+          }
         }
-      }
-    });
-    __syncthreads();
-    if (tid == 0 && s_cnt) s_base = atomicAdd(&S->small_n, min(s_cnt, (uint32_t)kSmallCap));
-    __syncthreads();
-    const uint32_t mine = min(s_cnt, (uint32_t)kSmallCap);
-    for (uint32_t q = tid; q < mine; q += kBlock)
-      if (s_base + q < (uint32_t)kSmallCap) st_agent(&a.W.small[s_base + q], sv[q]);
-  }
-  FC_TR(11);
-  // dense fix-up of this workgroup's range: q[idx] = +0 for every listed comp < T64.  Bins are
-  // in key order, so a candidate binned below beta is below T64 whatever T64 is: those are
-  // zeroed right after the gather ticket (zero_below, while T64 is being picked); once T64 is
-  // known only bin beta is left (fixup).  rank == 0: every candidate is slack (fixup alone).
-  const uint64_t imask = (1ull << a.ib) - 1;
-  auto bin_of = [&](uint64_t v) { return (((uint32_t)(v >> a.ib)) - t_lo) >> sbin; };
-  auto zero_below = [&]() {
-    for_cands(true, [&](const uint64_t (&v)[kGatherU]) {
+      });
+      __syncthreads();
+      if (tid == 0 && s_cnt) s_base = atomicAdd(&S->small_n, min(s_cnt, (uint32_t)kSmallCap));
+      __syncthreads();
+      const uint32_t mine = min(s_cnt, (uint32_t)kSmallCap);
+      for (uint32_t q = tid; q < mine; q += kBlock)
+        if (s_base + q < (uint32_t)kSmallCap) st_agent(&a.W.small[s_base + q], sv[q]);
+    }
+    FC_TR(11);
+    // dense: zero this range's candidates binned below beta (below T64 whatever it is); with
+    // rank == 0 every candidate is slack
+    const uint64_t imask = (1ull << a.ib) - 1;
+    if (a.dense && walk) {
+      const uint32_t below = rank > 0 ? beta : 0xffffffffu;
+      for_cands(rank > 0, [&](const uint64_t (&v)[kGatherU]) {
 #pragma unroll
-      for (int u = 0; u < kGatherU; ++u)
-        if (v[u] != ~0ull && bin_of(v[u]) < beta) a.dense[v[u] & imask] = 0.0f;
-    });
-  };
-  auto fixup = [&](uint64_t T, bool only_beta) {
-    for_cands(rank > 0, [&](const uint64_t (&v)[kGatherU]) {
-#pragma unroll
-      for (int u = 0; u < kGatherU; ++u)                  // ~0 (not a candidate) is never < T
-        if (v[u] < T && (!only_beta || bin_of(v[u]) == beta)) a.dense[v[u] & imask] = 0.0f;
-    });
-  };
-  const bool split_fix = a.dense && walk && !retry && rank > 0;   // (after the gather: v0 set)
-  // T64 from the gathered list: thread i ranks candidate i by counting the larger ones (comps
-  // are unique; <= 256 candidates) or, for a larger bin, an LDS bitonic sort
-  auto select_T = [&]() -> uint64_t {
-    if (retry) return 0ull;
-    if (a.k == 0) return kSelectNothing;
-    if (rank == 0) return ((uint64_t)t_hi + 1) << a.ib;  // exactly the definite set
-    __syncthreads();
-    if (cnt_beta <= (uint32_t)kBlock) {
+        for (int u = 0; u < kGatherU; ++u)
+          if (v[u] != ~0ull && bin_of(v[u]) < below) a.dense[v[u] & imask] = 0.0f;
+      });
+    }
+    if (!last_block_arrive_tree(a.W.tick + kTickWords, gridDim.x, blockIdx.x, &s_flag, 16)) return;
+    FC_TR(12);
+    // ---- last workgroup: T64 = the r_in-th largest of bin beta, the header, the dense slack of
+    // bin beta, self-cleaning ----
+    uint64_t T = 0;
+    uint32_t first_below = 0, list_n = 0;                 // sv[first_below, list_n): below T
+    bool sorted = false;
+    if (retry) {
+      T = 0;
+    } else if (a.k == 0) {
+      T = kSelectNothing;
+    } else if (rank == 0) {
+      T = ((uint64_t)t_hi + 1) << a.ib;                   // exactly the definite set
+    } else if (cnt_beta <= (uint32_t)kBlock) {
+      // thread i ranks candidate i by counting the larger ones (comps are unique)
       uint64_t mine = 0;
       if ((uint32_t)tid < cnt_beta) { mine = ld_agent(&a.W.small[tid]); sv[tid] = mine; }
       __syncthreads();
@@ -1331,59 +1285,43 @@ __global__ __launch_bounds__(kBlock) void k_resolve(ResolveArgs a0) {
         if (larger == r_in - 1) s_T = mine;
       }
       __syncthreads();
-      return s_T;
+      T = s_T;
+      list_n = cnt_beta;
+    } else {
+      uint32_t P2 = 1;
+      while (P2 < cnt_beta) P2 <<= 1;
+      for (uint32_t i = tid; i < P2; i += kBlock) sv[i] = i < cnt_beta ? ld_agent(&a.W.small[i]) : 0ull;
+      __syncthreads();
+      bitonic_desc(sv, P2);
+      T = sv[r_in - 1];
+      first_below = r_in; list_n = cnt_beta; sorted = true;
     }
-    uint32_t P2 = 1;
-    while (P2 < cnt_beta) P2 <<= 1;
-    for (uint32_t i = tid; i < P2; i += kBlock) sv[i] = i < cnt_beta ? ld_agent(&a.W.small[i]) : 0ull;
-    __syncthreads();
-    bitonic_desc(sv, P2);
-    return sv[r_in - 1];
-  };
-  const bool last = last_block_arrive_tree(a.W.tick + kTickWords, gridDim.x, blockIdx.x, &s_flag, 16);
-  if (last) {
-    // every workgroup has gathered: say so at once (dense: the others select T64 themselves
-    // from the same list instead of waiting for this one to sort and publish)
-    if (tid == 0 && a.dense) st_agent(&S->gen, gen0 + 1u);
-  } else {
-    if (!a.dense || !walk) return;
-    if (split_fix) zero_below();                        // while T64 is being picked
-    if (tid == 0) {                                     // relaxed sc1 poll (bounded)
-      uint32_t it = 0;
-      while (ld_agent(&S->gen) == gen0 && ++it < kSpinMax) __builtin_amdgcn_s_sleep(4);
-      s_st = it < kSpinMax ? 0u : 1u;
-      if (it >= kSpinMax) st_agent(&a.hdr->status, (uint32_t)FC_STATUS_TIMEOUT);
-    }
-    __syncthreads();
-    FC_TR(12);
-    if (s_st != 0) return;
-    const uint64_t T = select_T();
+    // another launch's timed-out wait (sticky err: the sample's pilot poll) makes the call retry
+    const bool other_err = ld_agent(&S->err) != 0u;
+    const uint32_t status = retry || other_err ? (uint32_t)FC_STATUS_RETRY_EXACT : (uint32_t)FC_STATUS_OK;
     FC_TR(14);
-    if (!retry) fixup(T, split_fix);
-    FC_TR(13);
-    return;
+    if (a.dense && status == FC_STATUS_OK && rank > 0) {
+      for (uint32_t i = (sorted ? first_below : 0u) + tid; i < list_n; i += kBlock) {
+        const uint64_t v = sv[i];
+        if (v < T) a.dense[v & imask] = 0.0f;
+      }
+    }
+    if (!rbin)                                            // the compaction's bins, for the next call
+      for (int b = tid; b < kHistBins; b += kBlock) a.W.chist[b] = 0;
+    if (tid == 0) {
+      a.hdr->thresh = T;
+      a.hdr->n_entries = n_ent;
+      if (status != FC_STATUS_OK) a.hdr->status = status;
+      a.hdr->n_definite = n_hi;
+      a.hdr->n_cand = n_cand;
+      S->small_n = 0; S->err = 0;
+      S->fz_seq += 1u;               // k_fused_mag: the next launch publishes fz_seq + 1
+    }
+    FC_TR(15);
   }
-  FC_TR(12);
-  // ---- last workgroup (nothing left to overlap: T64 first, then one full fix-up pass) ----
-  const uint64_t T = select_T();
-  // another workgroup's timed-out wait for the bins (sticky err) also makes the call retry
-  const bool other_err = ld_agent(&S->err) != 0u;
-  const uint32_t status = retry || other_err ? (uint32_t)FC_STATUS_RETRY_EXACT : (uint32_t)FC_STATUS_OK;
-  FC_TR(14);
-  if (a.dense && walk && !retry && !other_err) fixup(T, false);
-  if (!rbin)                                            // the compaction's bins, for the next call
-    for (int b = tid; b < kHistBins; b += kBlock) a.W.chist[b] = 0;
-  if (tid == 0) {
-    a.hdr->thresh = T;
-    a.hdr->n_entries = n_ent;
-    if (status != FC_STATUS_OK) a.hdr->status = status;
-    a.hdr->n_definite = n_hi;
-    a.hdr->n_cand = n_cand;
-    S->small_n = 0; S->err = 0;
-    S->fz_seq += 1u;               // k_fused_mag: the next launch publishes fz_seq + 1
-  }
-  FC_TR(15);
 }
+template __global__ void k_resolve<true>(ResolveArgs);
+template __global__ void k_resolve<false>(ResolveArgs);
 
 
 // --------------------------------------------------------------------------------------

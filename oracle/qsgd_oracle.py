@@ -13,8 +13,10 @@ with respect to the reference.  This module states the exact arithmetic the HIP 
 
     U_i   = h_i * 2**-16,  h_i = 16-bit half (i & 1) of linear word (i >> 1)
             (oracle/philox.py linear_words: one Philox block per 8 elements)
-    l_i   = floor(fl32(fl32(|g_i| * c) + U_i))   in [0, s];  0 if not finite,
-            c = fl32(fl64(s / norm));  if that overflows, the same in fp64 with c = fl64(s / norm)
+    l_i   = min(s, floor(fl32(|g_i| * c) + U_i))  (the sum exact, in fp64);  0 if NaN,
+            c = fl32(fl64(s / norm));  if that overflows, fl64(|g_i| * c) with c = fl64(s / norm)
+            (round 5: the sum used to be an fp32 round-to-nearest add, which could reach s + 1,
+            and a level above s was dropped to 0)
     code  = signbit(g_i) << (W - 1) | l_i,  W = 4 / 8 / 16 bits for bits <= 2 / 6 / 14
     value = fl32(+-(norm / (s * tau)) * l_i)         (fp64 product, one rounding)
 
@@ -44,23 +46,26 @@ def norm64(g: np.ndarray) -> float:
 
 
 def levels_and_signs(g: np.ndarray, bits: int, seed: int, offset: int, norm: float):
-    s = float(2 ** bits)
     n = g.shape[0]
     w = ph.linear_words((n + 1) // 2, seed, offset)
     h = (w[np.arange(n) >> 1] >> ((np.arange(n) & 1) * 16).astype(np.uint32)) & np.uint32(0xFFFF)
+    return levels_from_dither(g, h, bits, norm), np.signbit(g).astype(np.uint32)
+
+
+def levels_from_dither(g: np.ndarray, h: np.ndarray, bits: int, norm: float) -> np.ndarray:
+    """The levels for given 16-bit dither values h (U = h / 2**16)."""
+    s = float(2 ** bits)
     with np.errstate(invalid="ignore", divide="ignore", over="ignore"):
         c = s / norm if norm != 0.0 else math.inf            # fl64(s / norm), once
         c32 = np.float32(c)
-        if np.isfinite(c32):                                 # fp32 arithmetic
-            u = h.astype(np.float32) * np.float32(2.0 ** -16)
-            f = np.floor(np.abs(g.astype(np.float32)) * c32 + u)
+        u = h.astype(np.float64) * 2.0 ** -16                # exact
+        if np.isfinite(c32):                                 # fp32 product, exact sum
+            p = (np.abs(g.astype(np.float32)) * c32).astype(np.float64)
         else:                                                # s / norm above FLT_MAX
-            u = h.astype(np.float64) * 2.0 ** -16
-            f = np.floor(np.abs(g.astype(np.float64)) * c + u)
-    ok = np.isfinite(f) & (f >= 0) & (f <= s)
-    lev = np.where(ok, f, 0).astype(np.uint32)
-    sign = np.signbit(g).astype(np.uint32)
-    return lev, sign
+            p = np.abs(g.astype(np.float64)) * c
+        f = np.floor(p + u)
+        # NaN -> 0; the fp32 product may overshoot s (the exact s|g|/norm + U is < s + 1): s
+        return np.where(f >= 0, np.minimum(f, s), 0).astype(np.uint32)
 
 
 def encode(g: np.ndarray, bits: int, seed: int, offset: int, norm: float) -> np.ndarray:

@@ -465,13 +465,14 @@ def test_batch_encode_forked_streams(streams, groups):
 
 
 @pytest.mark.timeout(120)
-def test_batch_encodes_on_forked_streams_never_overlap():
-    """Two batched encodes must not run concurrently on one device: k_resolve's in-kernel waits
-    can then stall to the spin bound and the clients come back RETRY.  Without the per-device
-    ordering (codec._LAST_ENC) this loop — 2 x 64 clients of 4 M on two streams, steps queued
-    back to back with a FedAVG fold between them — hit it in 23 of 1,500 steps
-    (tools/stall_probe.py --off); with it, every status of 600 steps stays OK (counted on the
-    device after each step, no host sync)."""
+def test_batch_encodes_on_concurrent_streams_stay_ok():
+    """Two batched encodes running concurrently on one device (the sub-batches of
+    encode_top_batch(streams=2) on two forked streams, nothing orders them): no batched kernel
+    waits in-kernel, so no status ever leaves OK.  Round 4's k_resolve waited for the bin and
+    stalled here to the spin bound in 23 of 1,500 steps unless the encodes were serialized
+    (tools/stall_probe.py); this loop of 600 steps, queued back to back with a FedAVG fold
+    between them, counts the statuses on the device after each step (no host sync)."""
+    assert not hasattr(_codec(), "_ordered_encode")          # no serialization to lean on
     codec = _codec()
     from openmsftl_amd import _lib as L
     n, M, f = 1 << 22, 128, 0.1
@@ -952,6 +953,28 @@ def test_qsgd_fedavg_and_statistics():
     err = np.abs(acc / 200 - x / t)
     bound = 4 * qo.norm64(x) / (s4 * t) / np.sqrt(200)           # ~4 sigma of one level step
     assert (err < bound).mean() > 0.999
+
+
+@pytest.mark.parametrize("n", [1, 1000])
+def test_qsgd_one_hot_keeps_its_element(n):
+    """a one-hot gradient at bits = 14 lost its element (level s + 1 -> 0) about
+    once per 1024 encodes.  500 seeds: the codes equal the oracle's and the element always
+    decodes to +-norm / tau, never 0."""
+    from oracle import qsgd_oracle as qo
+    codec = _codec()
+    bits = 14
+    g = np.zeros(n, np.float32)
+    g[n // 2] = np.float32(-0.37)
+    gd = torch.from_numpy(g).cuda()
+    s = 2.0 ** bits
+    want_v = np.float32(-(qo.norm64(g) / (s * qo.tau(n, s))) * s)
+    for seed in range(500):
+        pkt = codec.encode_qsgd(gd, bits, seed=seed, offset=3)
+        h = pkt.header()
+        words = pkt.codes.cpu().numpy().view(np.uint32)
+        want = qo.encode(g, bits, seed, 3, h.p)
+        assert words[: want.shape[0]].tobytes() == want.tobytes()
+        assert codec.decode_qsgd(pkt).cpu().numpy()[n // 2] == want_v, seed
 
 
 def test_qsgd_compression_surface():

@@ -209,3 +209,23 @@ def test_qsgd_oracle_packing_and_scaling():
         s = 2.0 ** bits
         np.testing.assert_array_equal(np.abs(v), (nrm / (s * qo.tau(n, s)) * lev).astype(np.float32))
         assert np.array_equal(np.signbit(v) & (lev > 0), np.signbit(g) & (lev > 0))
+
+
+@pytest.mark.parametrize("bits", [1, 2, 8, 14])
+def test_qsgd_oracle_level_never_exceeds_s(bits):
+    """an element with |g_i| == ||g|| (a one-hot gradient) sits at level s for
+    every dither value U (floor(s + U) = s for U < 1); a level above s must never become 0.
+    All 65,536 dither values, at magnitudes whose fp32 product |g| * fl32(s / |g|) lands
+    above s as well as below it."""
+    from oracle import qsgd_oracle as qo
+    s = 2 ** bits
+    h = np.arange(65536, dtype=np.uint32)
+    for x in (1.0, 3.0, 0.1, 7.3e-5, 1e30, 2.9e-38):
+        x32 = np.float32(x)
+        lev = qo.levels_from_dither(np.full(65536, x32, np.float32), h, bits, float(x32))
+        assert (lev == s).all(), (x, np.unique(lev))
+    # below the top: floor(p + U) with the sum exact
+    g = np.full(65536, np.float32(0.5), np.float32)
+    lev = qo.levels_from_dither(g, h, bits, 1.0)
+    want = np.floor(np.float64(np.float32(0.5) * np.float32(s)) + h / 65536.0)
+    assert (lev == want).all()

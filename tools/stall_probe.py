@@ -1,6 +1,8 @@
-"""Concurrent batched encodes (encode_top_batch(streams=2)): count client statuses that are not
-OK over many steps, with the per-device serialization (codec._LAST_ENC) on or off.
-    python tools/stall_probe.py [--off] [--steps 300] [--n 4194304]"""
+"""Concurrent batched encodes (encode_top_batch(streams=2), the sub-batches free to overlap):
+count client statuses that are not OK over many steps.  Round 4's k_resolve waited in-kernel
+and stalled here (23 of 1,500 steps RETRY unless the encodes were serialized); since round 5
+no batched kernel waits, and no serialization exists to switch off.
+    python tools/stall_probe.py [--steps 300] [--n 4194304]"""
 import argparse
 import json
 import os
@@ -13,7 +15,6 @@ sys.path.insert(0, ROOT)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--off", action="store_true", help="disable the serialization (diagnosis)")
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--n", type=int, default=1 << 22)
     ap.add_argument("--m", type=int, default=128)
@@ -22,9 +23,6 @@ def main():
     import torch
     from openmsftl_amd import codec
     from openmsftl_amd.compression import kept_count
-    if args.off:
-        import contextlib
-        codec._ordered_encode = lambda dev: contextlib.nullcontext()
     n, M = args.n, args.m
     k = kept_count(0.1, n)
     import bench
@@ -52,7 +50,7 @@ def main():
     torch.cuda.synchronize()
     bad, bad_steps = int(bad), int(bad_steps)
     dt = (time.perf_counter() - t0) / args.steps
-    print(json.dumps({"serialized": not args.off, "n": n, "clients": M, "steps": args.steps,
+    print(json.dumps({"n": n, "clients": M, "steps": args.steps,
                       "steps_with_retry": bad_steps, "retry_statuses": bad,
                       "ms_per_step": round(dt * 1e3, 3)}), flush=True)
 
