@@ -70,7 +70,28 @@ def parse():
                          "timed step (exercises the rank-uniform exact re-encode)")
     ap.add_argument("--dump-agg", default=None,
                     help="test only: rank 0 saves the last step's aggregate (.npy) here")
+    ap.add_argument("--force-pg", action="store_true",
+                    help="initialise the process group and issue the step's collective even at "
+                         "one rank (tests the RCCL code path on a one-GPU box)")
     return ap.parse_args()
+
+
+def init_pg(dist, backend, world, rank, device, force=False) -> bool:
+    """The process group of this run: the launcher's env:// rendezvous for world > 1; with
+    ``force`` at world 1 a one-rank group on a free local port.  Returns whether one exists."""
+    if world <= 1 and not force:
+        return False
+    kw = {"device_id": device} if backend == "nccl" else {}
+    if world <= 1 and "MASTER_ADDR" not in os.environ:
+        import socket
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        dist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{port}", rank=0,
+                                world_size=1, **kw)
+    else:
+        dist.init_process_group(backend, **kw)
+    return True
 
 
 def spawn_ranks(argv, nproc, script=None):
@@ -278,14 +299,9 @@ def main():
         # rehearsal of the multi-rank path on fewer GPUs than ranks (ranks share devices; the
         # partial sums are staged through host memory, distributed.py); never the measurement
         local %= max(1, torch.cuda.device_count())
-    if world > 1:
-        torch.cuda.set_device(local)
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group("gloo")
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
+    pg = init_pg(dist, args.backend, world, rank, device, args.force_pg)
 
     from openmsftl_amd import _lib as L
     if args.lib:
@@ -314,7 +330,7 @@ def main():
     fold = packet_fold(pkts, views)
     jobs = codec.encode_jobs(grads, pkts)
     per_launch = 1 if args.no_batch else M          # clients per k_compact launch
-    fedavg = ShardedFedAvg(mode="reduce", dst=0)
+    fedavg = ShardedFedAvg(mode="reduce", dst=0, always_collective=args.force_pg)
     # two aggregate buffers: step i's RCCL reduce (async, on RCCL's stream) runs under step
     # i+1's encodes; step i+2 waits for it before folding into the same buffer again
     accs = [torch.empty(n, dtype=torch.float32, device=device) for _ in range(2)]
@@ -377,7 +393,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if pg:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -387,11 +403,11 @@ def main():
             poke[0] = rank == args.force_retry_rank and s == args.steps - 1
             step()
         torch.cuda.synchronize()
-    if world > 1:
+    if pg:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if pg:
         t = torch.tensor([elapsed], dtype=torch.float64,
                          device=device if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -404,7 +420,7 @@ def main():
     if args.dump_agg and rank == 0:
         import numpy as np
         np.save(args.dump_agg, accs[(nstep[0] - 1) & 1].cpu().numpy())
-    if world > 1:                                   # exact re-encodes over all ranks
+    if pg:                                          # exact re-encodes over all ranks
         t = torch.tensor([redo_total[0]], dtype=torch.int64,
                          device=device if args.backend == "nccl" else "cpu")
         dist.all_reduce(t)
@@ -458,6 +474,8 @@ def main():
                                "achieved_GBps": round(step_gbps, 1),
                                "frac": round(step_gbps / world / HBM_PEAK_GBPS, 4)}}
     extra["self_check"] = checked
+    extra["process_group"] = ({"backend": args.backend, "world": world,
+                               "collective_per_step": "reduce (async)"} if pg else None)
     if rank == 0 and not args.no_single:
         extra["single_gradient"] = single_gradient(torch, codec, grads[0], k, n)
         extra["qsgd_single_gradient"] = qsgd_single(torch, codec, grads[0], n)
@@ -496,7 +514,7 @@ def main():
             "roofline": roofline, "cpu_baseline": cpu, "extra": extra,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if pg:
         dist.destroy_process_group()
 
 
@@ -525,6 +543,7 @@ def single_gradient(torch, codec, g, k, n, iters=20):
         codec.compress_top_dense(g, k, out=out, packet=pkt, check=False)
     torch.cuda.synchronize()
     dt_d = (time.perf_counter() - t0) / iters
+    moved = dense_moved_bytes(n, pkt)
     codec.resolve([pkt])
     alg = 8.0 * n + 2 * ENTRY_BYTES * k
     return {"n": n, "k": k, "us_per_encode_decode": round(dt * 1e6, 1),
@@ -533,7 +552,17 @@ def single_gradient(torch, codec, g, k, n, iters=20):
             "hbm_frac": round(alg / dt / 1e9 / HBM_PEAK_GBPS, 4),
             "fused_dense": {"us": round(dt_d * 1e6, 1),
                             "alg_GBps": round(alg / dt_d / 1e9, 1),
-                            "hbm_frac": round(alg / dt_d / 1e9 / HBM_PEAK_GBPS, 4)}}
+                            "hbm_frac": round(alg / dt_d / 1e9 / HBM_PEAK_GBPS, 4),
+                            "moved_bytes": int(moved),
+                            "hbm_frac_moved": round(moved / dt_d / 1e9 / HBM_PEAK_GBPS, 4)}}
+
+
+def dense_moved_bytes(n, pkt):
+    """Bytes the drop-in dense top-k (fc_topk_encode_dense) actually moves, as opposed to
+    SURVEY §8(d)'s task bytes 8N + 16k (an encode AND a packet decode): it reads g (4N), writes
+    q (4N) and writes + re-reads the bracket's candidates (8 B each, the header's n_cand); the
+    sample (<= 8 MB) is left out."""
+    return 8.0 * n + 16.0 * pkt.header().n_cand
 
 
 def small_configs(torch, codec, L, device, f, n=16_777_216, M=128, steps=100):
@@ -609,10 +638,12 @@ def codec_matrix(torch, codec, L, device, n16=16_777_216, n25=25_557_032):
         us = _time_us(torch, lambda: (codec.encode_top(g, k, packet=pkt, check=False),
                                       codec.decode(pkt, out=out)))
         usd = _time_us(torch, lambda: codec.compress_top_dense(g, k, out=out, packet=pkt, check=False))
+        moved = dense_moved_bytes(n, pkt)
         assert codec.resolve([pkt]) == 0
         alg = 8.0 * n + 16.0 * k
         rows[name] = _row(us, alg, n=n, k=k, path="fc_topk_encode + fc_decode_dense",
-                          dense=_row(usd, alg, path="fc_topk_encode_dense"))
+                          dense=_row(usd, alg, path="fc_topk_encode_dense", moved_bytes=int(moved),
+                                     hbm_frac_moved=round(moved / usd / 1e3 / HBM_PEAK_GBPS, 4)))
     # rand f = 0.1 at 16 M: native Philox keys (fc_topk_encode PHILOX) and parity mode (the
     # host permutation as a bit mask -> fc_mask_encode idx/val -> decode)
     k = kept_count(0.1, n16)

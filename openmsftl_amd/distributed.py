@@ -59,10 +59,16 @@ def fedavg_weights(num_clients: int) -> np.ndarray:
 class ShardedFedAvg:
     """Per-rank fold + cross-rank combine of FedAVG partial sums."""
 
-    def __init__(self, mode: str = "reduce", dst: int = 0, group=None):
+    def __init__(self, mode: str = "reduce", dst: int = 0, group=None,
+                 always_collective: bool = False):
+        """``always_collective``: issue the reduce even in a world of one (an initialised
+        process group of one rank: RCCL's one-rank reduce is a device copy), so one GPU runs
+        the multi-GPU code path — the collective, its async work handle and its stream
+        ordering against the next encodes (bench.py / tools/e2e_bench.py ``--force-pg``)."""
         if mode not in ("reduce", "chain"):
             raise ValueError(f"mode must be 'reduce' or 'chain' (got {mode!r})")
         self.mode, self.dst, self.group = mode, dst, group
+        self.always_collective = always_collective
 
     def _staged(self, t) -> bool:
         """gloo group + device tensor: communicate through a host copy."""
@@ -93,6 +99,11 @@ class ShardedFedAvg:
         else:
             dist.recv(out, src=src, group=self.group)
 
+    @staticmethod
+    def _initialized() -> bool:
+        import torch.distributed as dist
+        return dist.is_available() and dist.is_initialized()
+
     def _world(self):
         import torch.distributed as dist
         if not dist.is_available() or not dist.is_initialized():
@@ -111,7 +122,8 @@ class ShardedFedAvg:
         if w.shape != (num_clients,):
             raise AssertionError("weights must have one entry per client")   # gar.py:41-42
         rows = shard_range(num_clients, world, rank)
-        if world == 1:
+        if world == 1 and not (self.always_collective and self.mode == "reduce"
+                               and self._initialized()):
             local_fold(rows, w[rows.start:rows.stop], out, False)
             return None if async_op else out
         if self.mode == "reduce":

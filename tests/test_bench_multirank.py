@@ -72,3 +72,63 @@ def test_world_mismatch_is_refused(tmp_path):
                           text=True, timeout=120)
     assert proc.returncode != 0
     assert "WORLD_SIZE" in proc.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_rccl_world1_bench_issues_its_reduce(tmp_path):
+    """The RCCL code path on a one-GPU box: bench.py --gpus 1 --backend
+    nccl --force-pg initialises a one-rank nccl group (device_id=), and every step issues its
+    one async reduce (the work handle waited on two steps later, stream-ordered against the
+    next encodes).  The aggregate equals the world-1 fold bit for bit (a one-rank sum-reduce
+    adds nothing) = the oracle's FedAVG of the rank's clients."""
+    agg = tmp_path / "agg.npy"
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--backend", "nccl",
+           "--force-pg", "--clients", str(M), "--n", str(N), "--steps", "4", "--warmup", "1",
+           "--no-cpu-baseline", "--no-single", "--no-matrix", "--roofline-steps", "0",
+           "--dump-agg", str(agg)]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(v, None)
+    proc = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert proc.returncode == 0, proc.stderr[-4000:]
+    lines = [ln for ln in proc.stdout.splitlines() if ln.startswith("{")]
+    line = json.loads(lines[-1])
+    assert line["n_gpus"] == 1
+    assert line["extra"]["process_group"] == {"backend": "nccl", "world": 1,
+                                              "collective_per_step": "reduce (async)"}
+    got = np.load(agg)
+    import bench
+    from openmsftl_amd.compression import kept_count
+    k = kept_count(F, N)
+    rows = []
+    for g in bench.make_grads(M, N, 0, torch.device("cuda", 0), torch):
+        idx, val = po.topk_packet(g.cpu().numpy(), k)
+        rows.append(po.decode_dense(N, idx, val))
+    want = go.sequential_weighted_sum(rows, np.full(M, 1.0 / M, np.float32))
+    assert got.tobytes() == want.tobytes()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_rccl_world1_e2e_reduce(tmp_path):
+    """tools/e2e_bench.py --gpus 1 --backend nccl --mode reduce --force-pg: the configs[4]
+    runner's reduce mode through a one-rank nccl group (the collective issued on the fold's
+    device buffer), on the committed configs[4] inputs: the aggregate digest equals the
+    oracle's (70 x 25.5 M, top f = 0.01)."""
+    import hashlib
+    from conftest import GOLDEN_DIR
+    d4 = json.load(open(os.path.join(GOLDEN_DIR, "digests_full.json")))["configs4"]
+    agg = tmp_path / "agg.npy"
+    cmd = [sys.executable, os.path.join(ROOT, "tools", "e2e_bench.py"), "--gpus", "1",
+           "--backend", "nccl", "--mode", "reduce", "--force-pg", "--source", "configs4",
+           "--group", "16", "--warmup", "0", "--reps", "1", "--dump-agg", str(agg)]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(v, None)
+    proc = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=280)
+    assert proc.returncode == 0, proc.stderr[-4000:]
+    line = json.loads([ln for ln in proc.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["process_group"] is True and line["backend"] == "nccl" and line["mode"] == "reduce"
+    got = np.load(agg)
+    assert hashlib.sha256(got.tobytes()).hexdigest() == d4["aggregate_sha256"]

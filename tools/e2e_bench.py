@@ -65,6 +65,8 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--source", default="synthetic", choices=("synthetic", "configs4"))
     ap.add_argument("--dump-agg", default=None, help="rank 0 saves the aggregate (.npy)")
+    ap.add_argument("--force-pg", action="store_true",
+                    help="a process group (and reduce mode's collective) even at one rank")
     return ap.parse_args(argv)
 
 
@@ -99,11 +101,8 @@ def main():
         local %= max(1, torch.cuda.device_count())
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    if world > 1:
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group("gloo")
+    import bench
+    pg = bench.init_pg(dist, args.backend, world, rank, dev, args.force_pg)
 
     from openmsftl_amd.compression import kept_count
     from openmsftl_amd.distributed import ShardedFedAvg, fedavg_weights
@@ -137,7 +136,7 @@ def main():
         rr = RankRing(pipe, dst=0)
         combine = lambda: rr.run(get, M, w)          # noqa: E731
     else:
-        sh = ShardedFedAvg(mode=args.mode, dst=0)
+        sh = ShardedFedAvg(mode=args.mode, dst=0, always_collective=args.force_pg)
         fold = host_fold(pipe, get)
         acc = torch.empty(n, dtype=torch.float32, device=dev)
         combine = lambda: sh.aggregate(fold, M, acc, weights=w)   # noqa: E731
@@ -150,7 +149,7 @@ def main():
 
     def barrier():
         torch.cuda.synchronize(dev)
-        if world > 1:
+        if pg:
             dist.barrier()
 
     for _ in range(args.warmup):
@@ -163,7 +162,7 @@ def main():
         barrier()
         times.append(time.perf_counter() - t)
     dt = min(times)
-    if world > 1:                                    # max over ranks of each rank's best
+    if pg:                                           # max over ranks of each rank's best
         tt = torch.tensor([dt, float(pipe.exact_fallbacks)], dtype=torch.float64)
         if args.backend == "nccl":
             tt = tt.to(dev)
@@ -181,7 +180,7 @@ def main():
     torch.cuda.synchronize(dev)
     h2d = reps * 4.0 * n / (time.perf_counter() - t) / 1e9
     h2d_all = [h2d]
-    if world > 1:
+    if pg:
         obj = [None] * world
         dist.all_gather_object(obj, h2d)
         h2d_all = obj
@@ -193,6 +192,7 @@ def main():
                           "cross-GPU combine -> D2H) GB/s",
                 "value": round(value, 2), "unit": "GB/s (client gradient bytes, all GPUs)",
                 "n_gpus": world, "mode": args.mode, "backend": args.backend,
+                "process_group": pg,
                 "seconds": round(dt, 4), "all_reps_s_rank0": [round(x, 4) for x in times],
                 "clients": M, "clients_per_gpu": M / world, "n": n, "k": k, "fraction": frac,
                 "group": args.group, "ring": args.ring, "h2d_GB": round(4.0 * n * M / 1e9, 2),
@@ -203,7 +203,7 @@ def main():
                 "config": "BASELINE configs[4]: %d clients x %d fp32, top f=%g, end-to-end"
                           % (M, n, frac)}
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if pg:
         dist.destroy_process_group()
 
 
