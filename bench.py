@@ -52,6 +52,7 @@ def parse():
     ap.add_argument("--roofline-steps", type=int, default=5,
                     help="extra encode passes with one stream, timed per launch for `roofline`")
     ap.add_argument("--lib", default=None, help="A/B only: load this libfedcodec.so build")
+    ap.add_argument("--tag", default=None, help="A/B only: a label echoed in the JSON line")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl (RCCL over xGMI: the measurement) or gloo (rehearsal only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -474,6 +475,8 @@ def main():
                                "achieved_GBps": round(step_gbps, 1),
                                "frac": round(step_gbps / world / HBM_PEAK_GBPS, 4)}}
     extra["self_check"] = checked
+    if args.tag is not None:
+        extra["tag"] = args.tag
     extra["process_group"] = ({"backend": args.backend, "world": world,
                                "collective_per_step": "reduce (async)"} if pg else None)
     if rank == 0 and not args.no_single:

@@ -97,6 +97,25 @@ static uint32_t decode_grid(uint64_t n, uint32_t per_cu = kDecBlocksPerCU) {
 #ifndef FC_SAMPLE_ROUNDS
 #define FC_SAMPLE_ROUNDS 4                        // sample groups per batched k_sample1 workgroup
 #endif
+// Candidate-histogram bins a batched encode's bracket is cut into: ~kCandPerBin expected
+// candidates per bin, 256..4096 bins.  Every batched resolve workgroup flushes that many
+// coalesced bins and the survivors of one bin are sorted on the chain, so fewer, fuller bins
+// suit a small gradient (configs[2], 16 M: ~120 K candidates -> 1024 bins, resolve 97 -> 86 us
+// per 128-client step) and 4096 a large one (128 M: ~465 K; 1024 bins made the batched
+// resolve slower, 151 -> 158 us per 64 clients, profiles/r05_ab_cand_bins.jsonl).  A lone
+// encode keeps 4096: its compaction bins every candidate with a device atomic, and fewer bins
+// queue more of them on one address (128 M packet encode 167 -> 277 us with 1024).
+#ifndef FC_CAND_PER_BIN
+#define FC_CAND_PER_BIN 128
+#endif
+static uint32_t cand_bins_log2(uint64_t n, const SamplePlan& P) {
+  if (P.full || P.lo_all || P.hi_none) return 12;
+  const double S = (double)P.nseg * 1024.0;
+  const double expect = (double)(P.r_lo - P.r_hi) * (double)n / S;   // candidates in the bracket
+  uint32_t lg = 8;
+  while (lg < 12 && (double)(1u << lg) * FC_CAND_PER_BIN < expect) ++lg;
+  return lg;
+}
 static SamplePlan make_plan(uint64_t n, uint64_t k, bool single = false) {
   SamplePlan P;
   memset(&P, 0, sizeof P);
@@ -122,6 +141,7 @@ static SamplePlan make_plan(uint64_t n, uint64_t k, bool single = false) {
     if (P.r_lo > (int64_t)S) P.lo_all = 1;
   }
   if (P.r_hi < 1) P.hi_none = 1;
+  P.cbins_log2 = 12;                 // lone encodes (fused in-kernel binning); batched: below
   // pilot (k_sample1): kPilotSegs segments spread over the sample, read by every workgroup.
   // Its ranks bracket the sample ranks scaled to the pilot, widened by 7 pilot sigmas + 8.
   P.pstride = (P.nseg + kSampleSegs - 1) / kSampleSegs;          // the sample grid
@@ -533,7 +553,8 @@ int fc_topk_encode_batch_part(const fc_encode_job* jobs, int m, uint64_t n, uint
   ra.W = ca.W; ra.jobs = jobs; ra.ws_stride = stride;
   ra.rbin = 1;                       // batched compaction: k_resolve bins the candidates
   hipStream_t s = (hipStream_t)stream;
-  const SamplePlan P = make_plan(n, k);
+  SamplePlan P = make_plan(n, k);
+  P.cbins_log2 = cand_bins_log2(n, P);
   // FC_SAMPLE_ROUNDS sample groups per workgroup (k_sample1): the same sample, fewer workgroups
   const dim3 sgrid((P.pstride + FC_SAMPLE_ROUNDS - 1) / FC_SAMPLE_ROUNDS, (uint32_t)m);
   if (part & FC_PART_SAMPLE) {

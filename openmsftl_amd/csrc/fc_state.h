@@ -128,6 +128,8 @@ struct SamplePlan {
   uint32_t np;         // pilot segments (<= kPilotSegs): workgroup 0's own segments
   uint32_t pstride;    // their spacing = the sample grid (segment j*pstride, j < np)
   int64_t pr_hi, pr_lo;  // pilot ranks (1-based from the top) that bound the fine window
+  uint32_t cbins_log2;   // candidate histogram bins used: the bracket's span >> sbin < 2^cbins_log2
+  uint32_t pad_;
 };
 #ifndef FC_SAMPLE_SEGS_PER_WG
 #define FC_SAMPLE_SEGS_PER_WG 4

@@ -191,8 +191,8 @@ __device__ __forceinline__ void seg_lane(const SamplePlan& P, uint32_t s, int ti
 // gh[b] += h[b] for the non-empty bins of a 4096-bin LDS histogram (256 threads).  (Two bins
 // per 64-bit atomic measured SLOWER: +10 us per lone encode, the last arriver's shard loads
 // queued behind the 64-bit atomics, profiles/r04_ab_sample_chain.jsonl.)
-__device__ __forceinline__ void flush_hist(uint32_t* gh, const uint32_t* h) {
-  for (int b = threadIdx.x; b < kHistBins; b += kBlock)
+__device__ __forceinline__ void flush_hist(uint32_t* gh, const uint32_t* h, uint32_t nb = kHistBins) {
+  for (uint32_t b = threadIdx.x; b < nb; b += kBlock)
     if (h[b]) atomicAdd(&gh[b], h[b]);
 }
 
@@ -392,7 +392,7 @@ __device__ __forceinline__ void sample_body(const T* __restrict__ g, const Sampl
   if (tid == 0) {
     const uint64_t span = (uint64_t)t_hi - t_lo;          // candidate keys: [t_lo, t_hi]
     uint32_t sb = 0;
-    while ((span >> sb) >= (uint64_t)kHistBins) ++sb;
+    while ((span >> sb) >= (1ull << P.cbins_log2)) ++sb;
     st_agent(&S->t_lo, t_lo); st_agent(&S->t_hi, t_hi); st_agent(&S->sbin, sb);
     st_agent(&S->L64, (uint64_t)t_lo << ib);
     st_agent(&S->cand_on, 1u);
@@ -1203,7 +1203,10 @@ __global__ __launch_bounds__(kBlock) void k_resolve(ResolveArgs a0) {
     });
     __syncthreads();
     FC_TR(29);
-    flush_hist(a.W.chist + (blockIdx.x % kCandShards) * kHistBins, h);   // this workgroup's shard
+    // only the bins the bracket's span uses (the sample sized sbin for 2^cbins_log2 of them:
+    // a batched launch flushes fewer coalesced atomics per workgroup)
+    const uint32_t nb = min((uint32_t)kHistBins, ((t_hi - t_lo) >> sbin) + 1u);
+    flush_hist(a.W.chist + (blockIdx.x % kCandShards) * kHistBins, h, nb);   // this workgroup's shard
     FC_TR(27);
     if (!last_block_arrive_tree(a.W.tick + 2 * kTickWords, gridDim.x, blockIdx.x, &s_flag)) return;
     // the last arriver sums the shards (every load first, then the clearing stores: their next
@@ -1215,7 +1218,8 @@ __global__ __launch_bounds__(kBlock) void k_resolve(ResolveArgs a0) {
 #pragma unroll
     for (int sh = 0; sh < kCandShards; ++sh)
 #pragma unroll
-      for (int j = 0; j < kPer; ++j) t[j] += ld_agent(&a.W.chist[sh * kHistBins + j * kBlock + tid]);
+      for (int j = 0; j < kPer; ++j)
+        if ((uint32_t)(j * kBlock + tid) < nb) t[j] += ld_agent(&a.W.chist[sh * kHistBins + j * kBlock + tid]);
 #pragma unroll
     for (int j = 0; j < kPer; ++j) h[j * kBlock + tid] = t[j];
     __syncthreads();
@@ -1224,8 +1228,8 @@ __global__ __launch_bounds__(kBlock) void k_resolve(ResolveArgs a0) {
       st_agent(&S->rb_beta, s_out[0]); st_agent(&S->rb_rin, s_out[1]);
       st_agent(&S->rb_cnt, h[s_out[0]]);
     }
-    for (int i = tid; i < kHistBins * kCandShards / 4; i += kBlock)
-      reinterpret_cast<uint4*>(a.W.chist)[i] = make_uint4(0u, 0u, 0u, 0u);
+    for (int sh = 0; sh < kCandShards; ++sh)
+      for (uint32_t b = tid; b < nb; b += kBlock) a.W.chist[sh * kHistBins + b] = 0u;
     FC_TR(28);
     return;
   } else {
