@@ -22,9 +22,10 @@ GAR (gar.py:44).  Here the rows never become a dense matrix on the common path:
   (``fc_weighted_sum_dense``); the GAR then reduces the merged rows.
 * 'qsgd' (opt-in) or a codec the reference rejects, float64 gradients (``RandomGaussian``
   with ``noise_scale == 0``, attack_models.py:105-106) and float64 GAR weights take the
-  generic path: the drop-in ``Compression`` per client in row order (same NumPy RNG draws as
-  the reference, the same exceptions at the same row), rows stacked on the device in G's
-  dtype, the same reductions in that dtype.
+  generic path: the drop-in ``Compression`` per client in row order on the device (same NumPy
+  RNG draws as the reference, the same exceptions at the same row), each row cast to G's dtype
+  and folded at once into the GAR's sum in NumPy's promoted dtype (``fold_rows``: one row of
+  device memory); only a merge (hierarchies) or a host GAR stacks the rows into G.
 
 ``aggregate_grads`` is a plain function so that :func:`openmsftl_amd.integration.install` can
 bind it onto the REFERENCE ``Aggregator`` class (its ``self.gar`` may then be a reference GAR
@@ -274,6 +275,38 @@ def merge_stages(G: torch.Tensor, sizes) -> torch.Tensor:
     return G
 
 
+def _client_row(C, grad, dev: torch.device):
+    """``C.compress(grad)`` (aggregation.py:63) as a device tensor: the drop-in Compression
+    gets the gradient on the device (no D2H of its result); another codec object gets the host
+    array it expects and its result is copied up."""
+    if isinstance(C, Compression) and not isinstance(grad, torch.Tensor):
+        a = np.asarray(grad)
+        if a.dtype in (np.float32, np.float64) and a.ndim == 1:
+            grad = torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    q = C.compress(grad)
+    if not isinstance(q, torch.Tensor):
+        q = torch.from_numpy(np.ascontiguousarray(q))
+    return q
+
+
+def fold_rows(gar, clients, n: int, tdt: torch.dtype, dev: torch.device) -> torch.Tensor:
+    """gar.py:44 over the rows aggregation.py:61-63 would stack, folded one row at a time as
+    each client's codec makes it (same NumPy RNG draws, same order; each row cast to G's dtype
+    ``tdt`` first, as ``G[ix, :] = q`` does): the +0-started row-order sum in NumPy's promoted
+    dtype of G and the GAR's (persisted) weights, without the M x N matrix."""
+    gdt = np.float64 if tdt == torch.float64 else np.float32
+    w = gar._weights(len(clients), gdt)
+    odt = torch.float64 if np.result_type(gdt, w.dtype) == np.float64 else torch.float32
+    wt = torch.from_numpy(np.ascontiguousarray(w))
+    acc = torch.empty(n, dtype=odt, device=dev)
+    row = torch.empty(n, dtype=tdt, device=dev)
+    for ix, c in enumerate(clients):
+        row.copy_(_client_row(c.C, c.grad, dev))        # G[ix, :] = q (cast to G's dtype)
+        codec.weighted_sum_dense([row], wt[ix:ix + 1], out=acc, out_dtype=odt,
+                                 continue_sum=ix > 0)
+    return acc
+
+
 def aggregate_grads(self, clients: List, input_feature: np.ndarray = None,
                     val_loader=None) -> None:
     """aggregation.py:54-78 on the device: sets ``self.agg_grad`` (host array) and
@@ -316,8 +349,15 @@ def aggregate_grads(self, clients: List, input_feature: np.ndarray = None,
     else:
         # generic codec mix / float64: the drop-in Compression per client, in row order; rows
         # take G's dtype (aggregation.py:61-63: G = zeros(..., dtype=clients[0].grad.dtype))
-        self.agg_path = "dense"
         tdt = torch.float64 if grad0.dtype == np.float64 else torch.float32
+        if device_gar and self.num_hierarchies == 0:
+            # nothing reads G but the GAR: fold each row as it is made (bounded: one row)
+            self.agg_path = "dense-fold"
+            self.curr_G = None
+            agg = fold_rows(self.gar, clients, n, tdt, dev)
+            self.agg_grad = agg.cpu().numpy()
+            return
+        self.agg_path = "dense"
         G = torch.empty((len(clients), n), dtype=tdt, device=dev)
         for ix, c in enumerate(clients):
             q = c.C.compress(c.grad)
@@ -353,7 +393,7 @@ class Aggregator:
         self.gar = self.__get_gar()
         self.curr_G = None
         self.agg_grad = None
-        self.agg_path = None                # "stream" | "dense": the path the last call took
+        self.agg_path = None                # "stream" | "dense-fold" | "dense": the last call's path
         self.analyze_pc = self.aggregation_config.get("pc_analysis", False)
         self.num_hierarchies = self.aggregation_config.get("num_hierarchies", 0)
         self.cluster_size_list = self.aggregation_config.get("cluster_size_list", [])

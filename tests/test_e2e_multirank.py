@@ -175,6 +175,74 @@ def test_rank_ring_two_gloo_ranks(M, group):
         assert res[("rows", r)] == mine
 
 
+def _rank_ring_plan_worker(rank, world, port, M, group, codec_name, q):
+    """RankRing with a row plan whose masks are drawn on the host: each rank draws every row's
+    mask in order (its own taken, the others dropped), so both ranks leave np.random where the
+    reference's one-process loop does."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from openmsftl_amd.aggregation import row_plan
+        from openmsftl_amd.compression import Compression
+        from openmsftl_amd.pipeline import HostFedAvg, RankRing
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        grads = _grads(M, seed=11)
+
+        class Client:
+            def __init__(self, g):
+                self.grad, self.C = g, Compression({"compression_function": codec_name,
+                                                    "dropout_p": 0.3, "fraction_coordinate": 0.1})
+        np.random.seed(5)
+        plan = row_plan([Client(g) for g in grads], N)
+        rr = RankRing(HostFedAvg(N, group=group, ring=2, device=dev, sets=2), dst=0)
+        out = rr.run(grads, M, plan=plan)
+        plan.close()
+        torch.cuda.synchronize()
+        q.put(("next", rank, int(np.random.randint(0, 2 ** 31 - 1))))
+        if rank == 0:
+            q.put(("agg", out.cpu().numpy().copy()))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(150)
+@pytest.mark.parametrize("codec_name", ["dropout-unbiased", "rand"])
+def test_rank_ring_two_gloo_ranks_host_draws(codec_name):
+    """The ring across two ranks with host-drawn masks ('dropout-unbiased' / 'rand' in parity
+    mode): the aggregate equals the one-process reference round (oracle) byte for byte and
+    every rank's RNG ends where the reference's does."""
+    import torch.multiprocessing as mp
+    from oracle import compression_oracle as co
+    M, group = 7, 2
+    grads = _grads(M, seed=11)
+    cfg = {"compression_function": codec_name, "dropout_p": 0.3, "fraction_coordinate": 0.1}
+    np.random.seed(5)
+    rows = [np.asarray(co.compress(cfg, g), np.float32) for g in grads]
+    nxt = int(np.random.randint(0, 2 ** 31 - 1))
+    want = go.FedAvgOracle({}).aggregate(np.stack(rows))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_ring_plan_worker, args=(r, 2, port, M, group, codec_name, q))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in range(3):
+            item = q.get(timeout=100)
+            res[item[0] if item[0] == "agg" else (item[0], item[1])] = item[-1]
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    assert res[("next", 0)] == nxt and res[("next", 1)] == nxt
+    assert res["agg"].tobytes() == want.tobytes()
+
+
 @pytest.mark.timeout(120)
 def test_aggregator_fans_out_over_devices():
     """The drop-in Aggregator with aggregation_config["devices"] = [0, 0]: a DeviceRing of two

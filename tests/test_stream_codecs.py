@@ -328,3 +328,39 @@ def test_aggregator_stream_draw_error_is_the_references():
     with pytest.raises(ValueError):
         agg.aggregate_grads([_Client(i, g, _RefCompression(c))
                              for i, (g, c) in enumerate(zip(grads, cfgs))])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["qsgd", "fp64", "f64_weights"])
+def test_aggregator_generic_path_folds_rows(kind):
+    """The generic path (codecs that do not stream: the opt-in QSGD; float64 gradients; float64
+    GAR weights) folds each row as the client's codec makes it, G never built: agg_grad equals
+    gar.py:44 on the G the rows would form (rows from Compression objects in the same state;
+    NumPy's promoted dtype)."""
+    torch = pytest.importorskip("torch")
+    from openmsftl_amd import Compression
+    from openmsftl_amd.aggregation import Aggregator
+    m, n = 6, 70_001
+    rng = np.random.default_rng(4)
+    if kind == "qsgd":
+        cfg = {"compression_function": "qsgd", "qsgd": "native", "num_bits": 2, "seed": 3}
+        grads = [rng.standard_normal(n).astype(np.float32) for _ in range(m)]
+    else:
+        cfg = {"compression_function": "dropout-unbiased", "dropout_p": 0.3}
+        grads = [rng.standard_normal(n).astype(np.float64 if kind == "fp64" else np.float32)
+                 for _ in range(m)]
+    gdt = grads[0].dtype
+    np.random.seed(9)
+    Cs = [Compression(cfg) for _ in range(m)]
+    rows = [np.asarray(Cs[i].compress(g), gdt) for i, g in enumerate(grads)]
+    nxt = int(np.random.randint(0, 2 ** 31 - 1))
+    w = np.full(m, 1.0 / m, np.float64 if kind == "f64_weights" else gdt)
+    want = np.sum(np.stack(rows) * w[:, None], axis=0)        # gar.py:44 (the reference's call)
+    agg = Aggregator({"aggregation_scheme": "fed_avg"})
+    agg.gar.gradient_weights = w
+    np.random.seed(9)
+    agg.aggregate_grads([_Client(i, g, Compression(cfg)) for i, g in enumerate(grads)])
+    assert int(np.random.randint(0, 2 ** 31 - 1)) == nxt
+    assert agg.agg_path == "dense-fold" and agg.curr_G is None
+    assert agg.agg_grad.dtype == want.dtype
+    assert agg.agg_grad.tobytes() == want.tobytes()
