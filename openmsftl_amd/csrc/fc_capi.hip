@@ -51,6 +51,7 @@ static WsPtrs ws_ptrs(void* ws, uint64_t n) {
   W.ehist = reinterpret_cast<uint32_t*>(b + L.off_ehist);
   W.chist = reinterpret_cast<uint32_t*>(b + L.off_chist);
   W.small = reinterpret_cast<uint64_t*>(b + L.off_small);
+  W.pub = reinterpret_cast<uint32_t*>(b + L.off_pub);
   W.ccnt = reinterpret_cast<uint32_t*>(b + L.off_status);
   W.cand = reinterpret_cast<uint64_t*>(b + L.off_cand);
   W.cand_cap = L.cand_cap;

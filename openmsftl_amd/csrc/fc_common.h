@@ -46,6 +46,17 @@ template <typename T>
 __device__ __forceinline__ void st_agent(T* p, T v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// 16-B record hand-off (one lane's dwordx4, 16-B aligned: one transaction each way): the
+// agent-scope (sc1) forms of a vector store and a load; the load waits for its data.
+typedef uint32_t fc_rec4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st16_agent(uint32_t* p, fc_rec4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" :: "v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ fc_rec4 ld16_agent(const uint32_t* p) {
+  fc_rec4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
 
 // ---- keys ----------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t mag_key(float x) {

@@ -17,8 +17,7 @@ struct alignas(16) TopkState {
   uint32_t err;          // sticky device error (spin timeout)
   uint32_t a_done, b_done, r_done;
   uint32_t pad0_[3];
-  uint32_t win_flag;     // k_sample1's fine window, published by workgroup 0: bit 31 valid,
-                         // level-1 bins hi << 12 | lo; reset by the sample's last block
+  uint32_t win_flag;     // (unused: k_fused_mag's window flags live in WsPtrs::pub)
   uint32_t pad1_[2];
   uint32_t t_lo, t_hi;   // bracket (keys): list key >= t_lo; candidates key <= t_hi
   uint32_t sbin;         // candidate histogram bin = (key - t_lo) >> sbin  (< 4096 bins)
@@ -26,8 +25,9 @@ struct alignas(16) TopkState {
   uint32_t small_n;      // survivors gathered for the LDS finish
   uint32_t e_shift, e_rank, e_matched, e_done, e_ticket, e_status;
   uint32_t gen;          // k_resolve generation: bumped when T64 is published (dense fix-up)
-  uint32_t fz_pub;       // k_fused_mag: the bracket is written (= fz_seq + 1 of that launch)
-  uint32_t fz_seq;       // k_fused_mag launches completed (bumped by the following k_resolve)
+  uint32_t fz_pub;       // (unused: k_fused_mag's bracket records live in WsPtrs::pub)
+  uint32_t fz_seq;       // k_fused_mag launches completed (bumped by the following k_resolve);
+                         // a launch tags its bracket records (fz_seq + 1) | bit 31
   uint32_t hgen;         // k_resolve: bumped once the bin beta below is published
   uint32_t rb_beta, rb_rin, rb_cnt;   // k_resolve: bin holding rank r, rank inside it, its count
   uint32_t pad_[3];
@@ -53,10 +53,19 @@ constexpr int kCandShards = FC_CAND_SHARDS;       // k_resolve's candidate histo
 constexpr int kTickGroups = 16;             // two-level last-arriver tickets (fc_common.h)
 constexpr int kTickStride = 64;             // u32 per ticket counter (one 256-B line each)
 constexpr int kTickWords = (kTickGroups + 1) * kTickStride;
+// k_fused_mag's in-launch publications, each written to several 128-B lines that their pollers
+// spread over (every poller on ONE line queued behind the others: ~900 chunk workgroups saw a
+// 16 M encode's bracket over a 5 us spread, then each read the state in a second round trip):
+//   bracket records: kPubCopies x {t_lo, t_hi, sbin, tag}, one 16-B store / load each
+//   window flags:    kWinCopies x the pilot's window word (k_sample1's win_flag format)
+constexpr int kPubCopies = 64;
+constexpr int kWinCopies = 16;
+constexpr int kPubStride = 32;              // u32 per copy (one 128-B line)
+constexpr int kPubWords = (kPubCopies + kWinCopies) * kPubStride;
 
 struct WsLayout {
   uint64_t nchunks, cand_cap;
-  uint64_t off_hist1, off_tick, off_ehist, off_chist, off_small, off_status, off_cand, bytes;
+  uint64_t off_hist1, off_tick, off_ehist, off_chist, off_small, off_pub, off_status, off_cand, bytes;
   __host__ __device__ static WsLayout of(uint64_t n) {
     WsLayout L;
     L.nchunks = (n + kChunk - 1) / kChunk;
@@ -73,6 +82,7 @@ struct WsLayout {
     o += 8192;
     L.off_chist = o;  o += 4ull * kHistBins * kCandShards;
     L.off_small = o;  o += 8ull * kSmallCap;
+    L.off_pub = o;    o += 4ull * kPubWords;        // n-independent, like every counter above
     L.off_status = o; o += 4ull * (L.nchunks ? L.nchunks : 1);   // per-chunk candidate counts
     o = (o + 15) & ~15ull;
     L.off_cand = o;   o += 8ull * L.cand_cap;
@@ -91,6 +101,7 @@ struct WsPtrs {
   TopkState* st;
   uint32_t *hist1, *tick, *ehist, *chist;   // hist1: kSampleShards x 4096; tick: 3 tickets
   uint64_t* small;
+  uint32_t* pub;           // k_fused_mag publications (kPubWords)
   uint32_t* ccnt;          // candidates per chunk (may exceed kCandSlot: overflowed chunk)
   uint64_t* cand;          // chunk c's candidates at [c * kCandSlot, + min(ccnt, kCandSlot))
   uint64_t cand_cap;
@@ -104,6 +115,7 @@ __device__ __forceinline__ WsPtrs ws_shift(WsPtrs W, uint64_t bytes) {
   W.ehist = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(W.ehist) + bytes);
   W.chist = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(W.chist) + bytes);
   W.small = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(W.small) + bytes);
+  W.pub = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(W.pub) + bytes);
   W.ccnt = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(W.ccnt) + bytes);
   W.cand = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(W.cand) + bytes);
   return W;

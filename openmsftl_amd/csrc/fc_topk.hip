@@ -276,7 +276,8 @@ struct SampleShared {
 
 // The body of k_sample1 for workgroup bid of nb (256 threads).  shared_pilot: a lone client's
 // launch (workgroup 0 publishes the window).  pub != 0 (k_fused_mag): once the bracket is
-// written, publish it to the compaction workgroups of the same launch (S->fz_pub = pub).
+// known, publish it to the compaction workgroups of the same launch (the kPubCopies bracket
+// records of W.pub, tag pub | bit 31).
 // SHARED_ONLY: the launch is a lone client's (the window always comes from workgroup 0's own
 // segments): no second set of pilot registers (k_fused_mag runs in 64 VGPRs)
 template <int KM, bool SHARED_ONLY = false, typename T = float>
@@ -320,14 +321,16 @@ __device__ __forceinline__ void sample_body(const T* __restrict__ g, const Sampl
   if (!shared_pilot || bid == 0) {
     F = pilot_window<KM, SHARED_ONLY, T>(g, P, seed, off, h, s_tmp, s_out, bid == 0, xs, es, ls);
     // publish the window as ONE sc1 word (its two level-1 bins, bit 31 = valid): the pollers'
-    // load returns the payload itself (a flag then three payload loads was one more round trip)
-    if (shared_pilot && tid == 0)
-      st_agent(&S->win_flag, 0x80000000u | ((F.khi >> 19) << 12) | (F.klo >> 19));
+    // load returns the payload itself (a flag then three payload loads was one more round trip);
+    // kWinCopies copies on their own lines, workgroup b polls copy b % kWinCopies
+    if (shared_pilot && tid < kWinCopies)
+      st_agent(&W.pub[(kPubCopies + tid) * kPubStride], 0x80000000u | ((F.khi >> 19) << 12) | (F.klo >> 19));
     for (int b = tid; b < kHistBins; b += kBlock) h[b] = 0;   // find_ranks_desc ended on a barrier
   } else {
     if (tid == 0) {                               // relaxed sc1 poll (bounded) of the payload
       uint32_t it = 0, w;
-      while (((w = ld_agent(&S->win_flag)) >> 31) == 0u && ++it < kSpinMax) __builtin_amdgcn_s_sleep(2);
+      const uint32_t* wf = &W.pub[(kPubCopies + bid % kWinCopies) * kPubStride];
+      while (((w = ld_agent(wf)) >> 31) == 0u && ++it < kSpinMax) __builtin_amdgcn_s_sleep(2);
       s_win[0] = w;
     }
     __syncthreads();
@@ -365,6 +368,10 @@ __device__ __forceinline__ void sample_body(const T* __restrict__ g, const Sampl
   if (!last_block_arrive_tree(W.tick, nb, bid, &sm.s_flag, 18)) return;
   FC_TR(5);
   // ---- last workgroup: the bracket (read + clear the histogram) ----
+  // the compaction's shard totals are reset first: wave 0's wait for its histogram loads below
+  // also drains these stores, so they precede the bracket's publication (pub) without a drain
+  // of their own
+  if (tid < kShards) { st_agent(&S->shard_ent[tid], 0u); st_agent(&S->shard_cnd[tid], 0u); }
   {
     // every load first (one round trip), then the clearing stores: a load and a store of the
     // same address issue in order, so interleaving them cost one round trip per bin (~45 us)
@@ -386,29 +393,33 @@ __device__ __forceinline__ void sample_body(const T* __restrict__ g, const Sampl
   FC_TR(23);
   const uint32_t t_hi = P.hi_none ? 0xffffffffu : fine_upper(s_out[0], F);
   const uint32_t t_lo = P.lo_all ? 0u : fine_lower(s_out[2], F);
-  // the state k_compact reads; sc1 stores from wave 0 so that a publication (pub) after its
-  // drain makes them visible to the compaction workgroups of the same launch on every XCD
-  if (tid < kShards) { st_agent(&S->shard_ent[tid], 0u); st_agent(&S->shard_cnd[tid], 0u); }
+  const uint64_t span = (uint64_t)t_hi - t_lo;            // candidate keys: [t_lo, t_hi]
+  uint32_t sb = 0;
+  while ((span >> sb) >= (1ull << P.cbins_log2)) ++sb;
+  // pub != 0 (k_fused_mag): the bracket to the compaction workgroups of this launch, one 16-B
+  // record per line (tag = pub | bit 31, never the previous launch's tag nor the zeroed start)
+  if (pub && tid < kPubCopies) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (the shard resets: long since done)
+    fc_rec4 r;
+    r.x = t_lo; r.y = t_hi; r.z = sb; r.w = pub | 0x80000000u;
+    st16_agent(&W.pub[tid * kPubStride], r);
+  }
   if (tid == 0) {
-    const uint64_t span = (uint64_t)t_hi - t_lo;          // candidate keys: [t_lo, t_hi]
-    uint32_t sb = 0;
-    while ((span >> sb) >= (1ull << P.cbins_log2)) ++sb;
     st_agent(&S->t_lo, t_lo); st_agent(&S->t_hi, t_hi); st_agent(&S->sbin, sb);
     st_agent(&S->L64, (uint64_t)t_lo << ib);
     st_agent(&S->cand_on, 1u);
     S->n_cand = 0; S->cand_over = 0; S->ent_over = 0;
-    S->win_flag = 0;               // (err: set by a timed-out wait, read and
-                                                  // cleared by this call's k_resolve)
-    if (pub) {                     // the compaction's state first: the header waits
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      st_agent(&S->fz_pub, pub);
-    }
+                                   // (err: set by a timed-out wait, read and cleared by this
+                                   // call's k_resolve)
     // the header's only writer in this launch: a static header written by workgroup 0 at its
     // start raced this store through another XCD's L2 (lower read back as 0).  Nothing in this
     // launch reads it (k_resolve does, after the kernel boundary).
     write_hdr_static(hdr, HI);
     hdr->lower = (uint64_t)t_lo << ib;
   }
+  // every sample workgroup has read its window copy (before its ticket): clear them for the next
+  // launch (plain stores, visible after this kernel's end-of-launch write-back)
+  if (shared_pilot && tid < kWinCopies) W.pub[(kPubCopies + tid) * kPubStride] = 0u;
   // clear the shards for the next call last, with plain 16-B stores (their next use is an
   // atomic in the next launch, after this kernel's end-of-launch write-back)
   for (uint32_t i = tid; i < (uint32_t)kHistBins * nsh / 4; i += kBlock)
@@ -961,9 +972,10 @@ __global__ __launch_bounds__(kCBlock, FC_MAG1_WAVES_PER_EU) void k_compact_mag1_
 // k_fused_mag: a lone client's k_sample1 + k_compact_mag1(_dense) in ONE launch.
 // Workgroups [0, nsamp) run the sample (256 of their 512 threads) and are dispatched first
 // (workgroups leave the dispatcher in order); every other workgroup is one chunk.  A chunk's
-// workgroup issues its loads, then waits (bounded relaxed sc1 poll) until the sample's last
-// workgroup publishes the bracket (S->fz_pub == fz_seq + 1, after its sc1 state stores have
-// drained), so the first resident round of chunk loads overlaps the sample's latency chain
+// workgroup issues its loads, then waits (bounded relaxed sc1 poll of one of the kPubCopies
+// 16-B bracket records, fc_state.h) until the sample's last workgroup has written them with the
+// tag (fz_seq + 1) | bit 31, so the first resident round of chunk loads overlaps the sample's
+// latency chain
 // instead of following it in a second launch.  fz_seq only changes in the k_resolve that
 // follows (stream order): every workgroup of this launch reads the same value.  The sample
 // never waits on a chunk workgroup, so no wait can deadlock; a timed-out one (never expected)
@@ -999,14 +1011,19 @@ __device__ __forceinline__ void fused_mag_wg(const CompactArgs& a0, const Sample
   float x[MagGeo<NW>::kQ];
   mag_load<NW>(a0.g, chunk, a0.n, x);
   FC_TR(24);
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0) {           // this workgroup's copy of the bracket record
+    const uint32_t* rec = &a0.W.pub[(blockIdx.x % kPubCopies) * kPubStride];
+    const uint32_t tag = pub | 0x80000000u;
     uint32_t it = 0;
-    while (ld_agent(&S->fz_pub) != pub && ++it < kSpinMax) __builtin_amdgcn_s_sleep(4);
+    fc_rec4 r = ld16_agent(rec);
+    while (r.w != tag && ++it < kSpinMax) {
+      __builtin_amdgcn_s_sleep(4);
+      r = ld16_agent(rec);
+    }
     if (it >= kSpinMax) st_agent(&S->err, 1u);
     MagState m;
-    m.L64 = ld_agent(&S->L64);
-    m.t_lo = ld_agent(&S->t_lo); m.t_hi = ld_agent(&S->t_hi);
-    m.cand_on = ld_agent(&S->cand_on); m.sbin = ld_agent(&S->sbin);
+    m.t_lo = r.x; m.t_hi = r.y; m.sbin = r.z; m.cand_on = 1u;
+    m.L64 = (uint64_t)r.x << a0.ib;   // = the sample's L64
     s_st = m;
   }
   __syncthreads();

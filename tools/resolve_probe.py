@@ -1,6 +1,6 @@
 """Encode-latency probe for A/B builds (tools/ab.py): the paths whose resolve / sample kernels
 changed between builds, each timed with HIP events over `--iters` back-to-back calls (best of
-`--reps`), plus the resolve-class kernel time (fc_timing, FC_TIME_ENGINE) per call.
+`--reps`), plus the resolve-, compaction- and decode-class kernel times (fc_timing) per call.
 
     python tools/resolve_probe.py [--lib PATH] [--tag T] [--iters 50] [--reps 3]
 
@@ -41,10 +41,10 @@ def main():
         for _ in range(3):
             fn()
         torch.cuda.synchronize()
-        best, best_res = None, None
+        best, best_res, best_k = None, None, None
         for _ in range(args.reps):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            with L.KernelTimer(L.FC_TIME_ENGINE if hasattr(L, "FC_TIME_ENGINE") else 4) as kt:
+            with L.KernelTimer(L.FC_TIME_ENGINE | L.FC_TIME_COMPACT | L.FC_TIME_DECODE) as kt:
                 e0.record()
                 for _ in range(iters):
                     fn()
@@ -54,8 +54,12 @@ def main():
             if best is None or us < best:
                 best = us
                 best_res = kt.ms.get("engine", 0.0) / iters * 1e3
+                best_k = {c: kt.ms.get(c, 0.0) / iters * 1e3 for c in ("compact", "decode")}
         res[name + "_us"] = round(best, 2)
         res[name + "_resolve_us"] = round(best_res, 2)
+        for c, v in best_k.items():
+            if v:
+                res[f"{name}_{c}_us"] = round(v, 2)
 
     gen = torch.Generator(device=dev)
     for n in (16_777_216, 134_217_728):
