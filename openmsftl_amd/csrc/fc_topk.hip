@@ -50,8 +50,35 @@ __device__ __forceinline__ uint32_t u4get(const uint4& v, int j) {
 }
 
 // Find the bin holding the rank1-th largest element (1-based, descending bins) of an LDS
-// histogram of kHistBins counts.  Result in s_out[0] = bin, s_out[1] = 1-based rank inside.
-// Requires a 256-thread workgroup.
+// histogram of kHistBins counts.  Result in s_out[0] = bin, s_out[1] = 1-based rank inside
+// (bin 0, rank 1 when rank1 is outside [1, total]).  256-thread workgroup; s_tmp[8]: the block
+// scan uses [0, 4), the owners [4, 8).  Thread t sums bins kHistBins-1-16t down 16; after the
+// scan the thread whose range holds the rank publishes (t, prefix), and one wave reads that
+// range's 16 bins one per lane and finds the bin with a 16-lane prefix sum and a ballot (the
+// owner walking its 16 bins through LDS was 16 dependent reads, ~1 us on the bracket's chain).
+__device__ __forceinline__ void rank_owner(uint32_t r, uint32_t excl, uint32_t sum, uint32_t total,
+                                           uint32_t* s_own) {
+  if (r >= 1 && r <= total && r > excl && r <= excl + sum) { s_own[0] = threadIdx.x; s_own[1] = excl; }
+  if (threadIdx.x == 0 && !(r >= 1 && r <= total)) s_own[0] = 0xffffffffu;
+}
+__device__ __forceinline__ void rank_in_owner(const uint32_t* h, uint32_t r, const uint32_t* s_own,
+                                              uint32_t* out) {
+  constexpr int per = kHistBins / kBlock;
+  const uint32_t lane = (uint32_t)lane_id();
+  const uint32_t ot = s_own[0];
+  if (ot == 0xffffffffu) {
+    if (lane == 0) { out[0] = 0; out[1] = 1; }
+    return;
+  }
+  const uint32_t oex = s_own[1];
+  const int otop = kHistBins - 1 - per * (int)ot;
+  const uint32_t hb = lane < (uint32_t)per ? h[otop - (int)lane] : 0u;
+  const uint32_t inc = wave_incl_scan(hb);
+  if (lane < (uint32_t)per && r > oex + inc - hb && r <= oex + inc) {   // exactly one lane
+    out[0] = (uint32_t)(otop - (int)lane);
+    out[1] = r - (oex + inc - hb);
+  }
+}
 __device__ void find_rank_desc(const uint32_t* h, uint32_t rank1, uint32_t* s_tmp,
                                uint32_t* s_out) {
   const int t = threadIdx.x;
@@ -60,23 +87,16 @@ __device__ void find_rank_desc(const uint32_t* h, uint32_t rank1, uint32_t* s_tm
   uint32_t sum = 0;
 #pragma unroll
   for (int b = 0; b < per; ++b) sum += h[top - b];
-  __syncthreads();                          // callers may still be reading s_out
-  if (t == 0) { s_out[0] = 0; s_out[1] = 1; }
+  uint32_t total;
+  const uint32_t excl = block_excl_scan(sum, s_tmp, &total);   // ends on a barrier
+  rank_owner(rank1, excl, sum, total, s_tmp + 4);
   __syncthreads();
-  const uint32_t excl = block_excl_scan(sum, s_tmp, nullptr);
-  if (rank1 > excl && rank1 <= excl + sum) {
-    uint32_t c = excl;
-    for (int b = 0; b < per; ++b) {
-      const uint32_t hb = h[top - b];
-      if (rank1 <= c + hb) { s_out[0] = (uint32_t)(top - b); s_out[1] = rank1 - c; break; }
-      c += hb;
-    }
-  }
+  if (t < 64) rank_in_owner(h, rank1, s_tmp + 4, s_out);
   __syncthreads();
 }
 
-// Both ranks of find_rank_desc in one scan: s_out[0..1] for r1, s_out[2..3] for r2 (bin 0,
-// rank 1 when a rank is outside [1, total]).  256-thread workgroup; 2 barriers + 1.
+// Both ranks of find_rank_desc in one scan: s_out[0..1] for r1 (wave 0), s_out[2..3] for r2
+// (wave 1).  256-thread workgroup.
 __device__ void find_ranks_desc(const uint32_t* h, uint32_t r1, uint32_t r2, uint32_t* s_tmp,
                                 uint32_t* s_out) {
   const int t = threadIdx.x;
@@ -87,21 +107,11 @@ __device__ void find_ranks_desc(const uint32_t* h, uint32_t r1, uint32_t r2, uin
   for (int b = 0; b < per; ++b) sum += h[top - b];
   uint32_t total;
   const uint32_t excl = block_excl_scan(sum, s_tmp, &total);
-  // the bins are re-read from LDS (only the one thread whose range holds r walks them): 16
-  // live histogram registers pushed k_fused_mag's sample part into scratch
-  auto find = [&](uint32_t r, int o) {
-    if (r > excl && r <= excl + sum) {
-      uint32_t c = excl;
-      for (int b = 0; b < per; ++b) {
-        const uint32_t hb = h[top - b];
-        if (r <= c + hb) { s_out[o] = (uint32_t)(top - b); s_out[o + 1] = r - c; break; }
-        c += hb;
-      }
-    }
-    if (t == 0 && !(r >= 1 && r <= total)) { s_out[o] = 0; s_out[o + 1] = 1; }
-  };
-  find(r1, 0);
-  find(r2, 2);
+  rank_owner(r1, excl, sum, total, s_tmp + 4);
+  rank_owner(r2, excl, sum, total, s_tmp + 6);
+  __syncthreads();
+  if (t < 64) rank_in_owner(h, r1, s_tmp + 4, s_out);
+  else if (t < 128) rank_in_owner(h, r2, s_tmp + 6, s_out + 2);
   __syncthreads();
 }
 
@@ -1009,6 +1019,11 @@ __device__ __forceinline__ void fused_mag_wg(const CompactArgs& a0, const Sample
   // the batched pass interleaves clients, measured 147 -> 155 / 164 us for a 128 M packet)
   const uint32_t chunk = blockIdx.x - nsamp;
   float x[MagGeo<NW>::kQ];
+  // the first resident round (chunk < 1024) starts its loads ~2.4 us late (s_sleep 90 x 64
+  // clocks), so that the sample's loads are not queued behind 32 MB of chunk loads; those still
+  // arrive long before the bracket (~14 us at 16 M).  16 M dense fused kernel 38.7 -> 37.6 us,
+  // 128 M packet 140.5 -> 138 us (profiles/r05_ab_fused_publish_find_delay.jsonl)
+  if (chunk < 1024u) __builtin_amdgcn_s_sleep(90);
   mag_load<NW>(a0.g, chunk, a0.n, x);
   FC_TR(24);
   if (threadIdx.x == 0) {           // this workgroup's copy of the bracket record

@@ -57,7 +57,20 @@ def main():
             if col.size:
                 res[name][sl] = [round(float(col.min()), 2), round(float(np.median(col)), 2),
                                  round(float(col.max()), 2), int(col.size)]
-    print(json.dumps({"n": n, "dense": args.dense, "phases_us_min_med_max_count": res}), flush=True)
+    # k_fused_mag's chunk workgroups split into those that had loaded before the bracket was
+    # published (slot 6: the first resident round) and the later ones
+    rounds = {}
+    t6 = t[:, 6].max()
+    t0 = t[t[:, 0] > 0, 0].min() if (t[:, 0] > 0).any() else 0.0
+    ck = (t[:, 24] > 0) & (t[:, 26] > 0)
+    if t6 > 0 and ck.any():
+        for nm, sel in (("early", ck & (t[:, 24] <= t6)), ("late", ck & (t[:, 24] > t6))):
+            if sel.any():
+                rounds[nm] = {int(sl): [round(float(np.percentile(t[sel, sl] - t0, q)), 2) for q in (0, 10, 50, 90, 100)]
+                              for sl in (24, 25, 26)}
+                rounds[nm]["count"] = int(sel.sum())
+    print(json.dumps({"n": n, "dense": args.dense, "phases_us_min_med_max_count": res,
+                      "fused_rounds_p0_10_50_90_100": rounds}), flush=True)
 
 
 if __name__ == "__main__":
