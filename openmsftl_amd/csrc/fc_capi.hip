@@ -233,8 +233,17 @@ static int launch_engine(int key_mode, const EngineArgs& base, int passes, hipSt
 
 // top-k compaction: k_compact_mag1, one workgroup per (chunk, client).  (Measured slower
 // and dropped: a persistent LDS-DMA ring, 1.5x; one wave per chunk, 1.1x — DESIGN.md §Lessons.)
+// (mag_item_of: a 3-D grid of interleave groups, or a linear one past the grid's y limit)
+static dim3 compact_mag_grid(CompactArgs& a, uint32_t m) {
+  a.m = m;
+  const uint32_t il = m < (uint32_t)FC_MAG1_IL ? m : (uint32_t)FC_MAG1_IL;
+  a.grid3 = a.nchunks <= 65535u ? 1u : 0u;
+  return a.grid3 ? dim3(il, a.nchunks, (m + il - 1) / il) : dim3(a.nchunks, m);
+}
 static void launch_compact_mag(const CompactArgs& a, uint32_t m, hipStream_t s) {
-  hipLaunchKernelGGL(k_compact_mag1, dim3(a.nchunks, m), dim3(kCBlock), 0, s, a);
+  CompactArgs b = a;
+  const dim3 grid = compact_mag_grid(b, m);
+  hipLaunchKernelGGL(k_compact_mag1, grid, dim3(kCBlock), 0, s, b);
 }
 
 // the PredArgs of k_compact_pred from a compaction's CompactArgs
@@ -502,7 +511,8 @@ int fc_topk_encode_dense(const float* g, uint64_t n, uint64_t k, uint16_t* idx, 
     rc = launch_sample(FC_KEY_MAGNITUDE, dim3(sgrid), g, P, 0ull, 0ull, ca.W, ca.ib, hdr, hi, nullptr, 0ull, s);
     if (rc) return rc;
     TimedLaunch t(FC_TIME_COMPACT, s);
-    hipLaunchKernelGGL(k_compact_mag1_dense, dim3(ca.nchunks, 1), dim3(kCBlock), 0, s, ca);
+    const dim3 grid = compact_mag_grid(ca, 1);
+    hipLaunchKernelGGL(k_compact_mag1_dense, grid, dim3(kCBlock), 0, s, ca);
     FC_LAUNCHED("k_compact_mag1_dense");
   }
   // k_resolve publishes T64 to its own workgroups, which then zero the slack in q

@@ -172,6 +172,10 @@ typedef uint32_t fc_u32x8 __attribute__((ext_vector_type(8)));
 // each one (4 serial HBM latencies per chunk).  Callers check bounds once per chunk.
 typedef float fc_f4v __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) const fc_f4v fc_gf4v;
+// GLOBAL address space for pointers that come out of memory (job tables, row / view arrays):
+// as generic pointers their loads and stores are flat_ ops, which also count in lgkmcnt, so the
+// next scalar-load or LDS wait waits for them too
+#define FC_G __attribute__((address_space(1)))
 __device__ __forceinline__ float4 load4_full(const float* p) {
   const fc_f4v v = __builtin_nontemporal_load((fc_gf4v*)p);
   return make_float4(v.x, v.y, v.z, v.w);

@@ -938,10 +938,18 @@ __global__ __launch_bounds__(kBlock) void k_wsum(const float* const* rows, const
       }
     }
     for (int r = 0; r < m; ++r) {
-      const float* row = rows[r];
+      const FC_G float* row = (const FC_G float*)rows[r];   // (global: rows come from memory)
       float4 x;
       if (((uintptr_t)row & 15) == 0) {        // rows of an (M, N) G with N % 4 != 0 are not
-        x = load4(row, e, n);                   // 16-B aligned: wave-uniform scalar fallback
+        if (e + 4 <= n) {                       // 16-B aligned: wave-uniform scalar fallback
+          const fc_f4v v = __builtin_nontemporal_load((fc_gf4v*)(row + e));
+          x = make_float4(v.x, v.y, v.z, v.w);
+        } else {
+          x.x = e + 0 < n ? row[e + 0] : 0.f;
+          x.y = e + 1 < n ? row[e + 1] : 0.f;
+          x.z = e + 2 < n ? row[e + 2] : 0.f;
+          x.w = 0.f;
+        }
       } else {
         x.x = e + 0 < n ? row[e + 0] : 0.f;
         x.y = e + 1 < n ? row[e + 1] : 0.f;

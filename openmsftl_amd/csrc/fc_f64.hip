@@ -71,27 +71,11 @@ __device__ void bitonic_desc128(u128* sv, uint32_t P2) {
   }
 }
 
-// Rank-from-the-top bin of an LDS histogram (256 threads): see fc_topk.hip find_rank_desc.
-__device__ void find_rank_desc64(const uint32_t* h, uint32_t rank1, uint32_t* s_tmp, uint32_t* s_out) {
-  const int t = threadIdx.x;
-  constexpr int per = kHistBins / kBlock;
-  const int top = kHistBins - 1 - per * t;
-  uint32_t sum = 0;
-#pragma unroll
-  for (int b = 0; b < per; ++b) sum += h[top - b];
-  __syncthreads();
-  if (t == 0) { s_out[0] = 0; s_out[1] = 1; }
-  __syncthreads();
-  const uint32_t excl = block_excl_scan(sum, s_tmp, nullptr);
-  if (rank1 > excl && rank1 <= excl + sum) {
-    uint32_t c = excl;
-    for (int b = 0; b < per; ++b) {
-      const uint32_t hb = h[top - b];
-      if (rank1 <= c + hb) { s_out[0] = (uint32_t)(top - b); s_out[1] = rank1 - c; break; }
-      c += hb;
-    }
-  }
-  __syncthreads();
+// Rank-from-the-top bin of an LDS histogram (256 threads): fc_topk.hip's find_rank_desc (one
+// wave searches the owning thread's 16 bins).
+__device__ __forceinline__ void find_rank_desc64(const uint32_t* h, uint32_t rank1, uint32_t* s_tmp,
+                                                 uint32_t* s_out) {
+  find_rank_desc(h, rank1, s_tmp, s_out);
 }
 
 // One radix pass (or the final collect + LDS sort) of the k-th largest 95-bit comp.

@@ -92,6 +92,15 @@ __global__ __launch_bounds__(64) void k_write_hdr(fc_packet_hdr* hdr, HdrInit HI
 // both let hipcc merge the two load forms into per-lane 64-bit addresses without the NT hint.)
 template <int SRC, int FMT, bool FULL>
 __device__ __forceinline__ void pred_body(const PredArgs& a, uint32_t chunk, PredShared& sh) {
+  // the packet / workspace pointers in the GLOBAL address space (fc_topk.hip MagOut: generic
+  // ones, taken from the job table, made every store a flat_store that the next LDS wait waited on)
+  FC_G uint16_t* const a_idx = (FC_G uint16_t*)a.idx;
+  FC_G float* const a_val = (FC_G float*)a.val;
+  FC_G uint32_t* const a_bitmap = (FC_G uint32_t*)a.bitmap;
+  FC_G uint32_t* const a_cnt = (FC_G uint32_t*)a.cnt;
+  FC_G uint64_t* const a_qoff = (FC_G uint64_t*)a.qoff;
+  FC_G uint32_t* const a_ccnt = (FC_G uint32_t*)a.ccnt;
+  FC_G uint64_t* const a_cand = (FC_G uint64_t*)a.cand;
   constexpr int NW = kCWaves, NQ = MagGeo<NW>::kQ, NI = NQ / 4;
   static_assert(NQ == 16, "16 elements per lane");
   const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
@@ -208,14 +217,14 @@ __device__ __forceinline__ void pred_body(const PredArgs& a, uint32_t chunk, Pre
     const uint64_t m = __ballot(p);
     const uint32_t pos = prefix_count(m) + goff_of(q);
     if (FMT == FC_FMT_BITMAP && lane < 2)          // the group's two bitmap words
-      a.bitmap[(base + FC_LOC(q) - (uint32_t)lane) / 32 + (uint32_t)lane] = (uint32_t)(m >> (32 * lane));
+      a_bitmap[(base + FC_LOC(q) - (uint32_t)lane) / 32 + (uint32_t)lane] = (uint32_t)(m >> (32 * lane));
     const float v = ((nb >> q) & 1u) ? __uint_as_float(0x7fc00000u) : x[q];
     if (p) {
       if (staged) {
         sh.st[pos] = make_uint2(FC_LOC(q), __float_as_uint(v));
       } else {
-        if (FMT == FC_FMT_IDXVAL) a.idx[slot + pos] = (uint16_t)FC_LOC(q);
-        a.val[slot + pos] = v;
+        if (FMT == FC_FMT_IDXVAL) a_idx[slot + pos] = (uint16_t)FC_LOC(q);
+        a_val[slot + pos] = v;
       }
     }
   }
@@ -254,11 +263,11 @@ __device__ __forceinline__ void pred_body(const PredArgs& a, uint32_t chunk, Pre
     c_ovf |= wn[j] > (uint32_t)kCW;
   }
   if (tid == 0) {
-    a.cnt[chunk] = tot_e;
-    if (FMT == FC_FMT_IDXVAL && a.qoff)
-      a.qoff[chunk] = qs1 | ((uint64_t)qs2 << 16) | ((uint64_t)qs3 << 32) | ((uint64_t)tot_e << 48);
+    a_cnt[chunk] = tot_e;
+    if (FMT == FC_FMT_IDXVAL && a_qoff)
+      a_qoff[chunk] = qs1 | ((uint64_t)qs2 << 16) | ((uint64_t)qs3 << 32) | ((uint64_t)tot_e << 48);
     if (SRC == kSrcPhiloxKey) {
-      a.ccnt[chunk] = c_ovf ? max(tot_c, (uint32_t)kCandSlot + 1u) : tot_c;
+      a_ccnt[chunk] = c_ovf ? max(tot_c, (uint32_t)kCandSlot + 1u) : tot_c;
       atomicAdd(&a.S->shard_ent[chunk % kShards], tot_e);
       if (tot_c) atomicAdd(&a.S->shard_cnd[chunk % kShards], tot_c);
     }
@@ -269,12 +278,12 @@ __device__ __forceinline__ void pred_body(const PredArgs& a, uint32_t chunk, Pre
         const uint4 p0 = *reinterpret_cast<const uint4*>(&sh.st[t]);
         const uint4 p1 = *reinterpret_cast<const uint4*>(&sh.st[t + 2]);
         if (FMT == FC_FMT_IDXVAL)
-          *reinterpret_cast<uint2*>(a.idx + slot + t) = make_uint2(p0.x | (p0.z << 16), p1.x | (p1.z << 16));
-        *reinterpret_cast<uint4*>(a.val + slot + t) = make_uint4(p0.y, p0.w, p1.y, p1.w);
+          *(FC_G fc_u32x2*)(a_idx + slot + t) = fc_u32x2{p0.x | (p0.z << 16), p1.x | (p1.z << 16)};
+        *(FC_G fc_u32x4*)(a_val + slot + t) = fc_u32x4{p0.y, p0.w, p1.y, p1.w};
       } else {
         for (uint32_t u = t; u < tot_e; ++u) {
-          if (FMT == FC_FMT_IDXVAL) a.idx[slot + u] = (uint16_t)sh.st[u].x;
-          a.val[slot + u] = __uint_as_float(sh.st[u].y);
+          if (FMT == FC_FMT_IDXVAL) a_idx[slot + u] = (uint16_t)sh.st[u].x;
+          a_val[slot + u] = __uint_as_float(sh.st[u].y);
         }
       }
     }
@@ -288,7 +297,7 @@ __device__ __forceinline__ void pred_body(const PredArgs& a, uint32_t chunk, Pre
       if ((uint32_t)j < wj) pre += m;
       if ((uint32_t)j == wj) nj = m;
     }
-    if (p < nj) a.cand[(uint64_t)chunk * kCandSlot + pre + p] = sh.cst[tid];
+    if (p < nj) a_cand[(uint64_t)chunk * kCandSlot + pre + p] = sh.cst[tid];
   }
 }
 

@@ -210,18 +210,36 @@ __device__ __forceinline__ void flush_hist(uint32_t* gh, const uint32_t* h, uint
 // float32: the values themselves.  float64 (fc_topk_dense_f64's sampled path, fc_f64.hip): the
 // 31-bit HIGH key of each double (|x| bits >> 32: exponent + 20 mantissa bits) as a float bit
 // pattern, so mag_key of it is that high key (clamped at kNanKey: a non-decreasing map, which is
-// all a bracket needs).
-__device__ __forceinline__ float4 load4_sample(const float* __restrict__ g, uint64_t e, uint64_t n) {
-  return load4_plain(g, e, n);
+// all a bracket needs).  Through the GLOBAL address space: a batched launch takes g from the job
+// table, and hipcc made the generic pointer's loads flat_loads, which count in lgkmcnt too, so
+// the scalar loads between segments waited for each segment's data (4 serial round trips per
+// sample group instead of one).
+typedef __attribute__((address_space(1))) const float fc_gfloat;
+typedef __attribute__((address_space(1))) const double fc_gdouble;
+typedef double fc_d2v __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(1))) const fc_d2v fc_gd2v;
+__device__ __forceinline__ float4 load4_sample(const float* __restrict__ g0, uint64_t e, uint64_t n) {
+  fc_gfloat* g = (fc_gfloat*)g0;
+  if (e + 4 <= n) {
+    const fc_f4v v = *(fc_gf4v*)(g + e);
+    return make_float4(v.x, v.y, v.z, v.w);
+  }
+  float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (e + 0 < n) r.x = g[e + 0];
+  if (e + 1 < n) r.y = g[e + 1];
+  if (e + 2 < n) r.z = g[e + 2];
+  if (e + 3 < n) r.w = g[e + 3];
+  return r;
 }
 __device__ __forceinline__ float hikey_f(double x) {
   return __uint_as_float((uint32_t)(((uint64_t)__double_as_longlong(x) & 0x7fffffffffffffffull) >> 32));
 }
-__device__ __forceinline__ float4 load4_sample(const double* __restrict__ g, uint64_t e, uint64_t n) {
+__device__ __forceinline__ float4 load4_sample(const double* __restrict__ g0, uint64_t e, uint64_t n) {
+  fc_gdouble* g = (fc_gdouble*)g0;
   double v[4] = {0.0, 0.0, 0.0, 0.0};
   if (e + 4 <= n) {
-    const double2 a = *reinterpret_cast<const double2*>(g + e);
-    const double2 b = *reinterpret_cast<const double2*>(g + e + 2);
+    const fc_d2v a = *(fc_gd2v*)(g + e);
+    const fc_d2v b = *(fc_gd2v*)(g + e + 2);
     v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
   } else {
 #pragma unroll
@@ -486,6 +504,8 @@ struct CompactArgs {
   const fc_encode_job* jobs;   // batched encode: client blockIdx.y overrides g / packet / W
   uint64_t ws_stride;
   float* dense;             // fc_topk_encode_dense: also stream q = listed ? g : +0 (one client)
+  uint32_t grid3;           // k_compact_mag1(_dense): 3-D grid (clients of a group, chunks, groups)
+  uint32_t m;               // its clients (the last group may be partial)
 };
 
 // Per-client fields of a batched launch (jobs[blockIdx.y]); no-op for a single client.
@@ -584,19 +604,22 @@ __device__ __forceinline__ void mag_exact_bits(const MagPred& P, float (&x)[MagG
 }
 
 // Output / workspace pointers of one item (client), built when the item is compacted: the
-// full CompactArgs of two items live across the loop spilled ~130 SGPRs.
+// full CompactArgs of two items live across the loop spilled ~130 SGPRs.  The data pointers are
+// GLOBAL-address-space: a batched launch reads them from the job table, and as generic pointers
+// hipcc made every packet store a flat_store, which also counts in lgkmcnt, so each wave's next
+// LDS read waited for its packet stores (and wave 0 for the chunk's counts) to complete.
 struct MagOut {
-  const float* g;
-  uint16_t* idx;
-  float* val;
-  uint32_t* cnt;
-  uint64_t* qoff;
+  const FC_G float* g;
+  FC_G uint16_t* idx;
+  FC_G float* val;
+  FC_G uint32_t* cnt;
+  FC_G uint64_t* qoff;
   TopkState* S;
-  uint32_t* ccnt;
-  uint64_t* cand;
-  uint32_t* chist;
+  FC_G uint32_t* ccnt;
+  FC_G uint64_t* cand;
+  uint32_t* chist;          // (atomics)
   uint32_t ib;
-  float* dense;             // nullptr unless fc_topk_encode_dense
+  FC_G float* dense;        // nullptr unless fc_topk_encode_dense
 };
 
 // PKT = false (the drop-in dense path, fc_topk_encode_dense): q is the product, the packet
@@ -758,8 +781,8 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
         iv.x = p0.x | (p0.z << 16); iv.y = p1.x | (p1.z << 16);
         fc_u32x4 vv;
         vv.x = p0.y; vv.y = p0.w; vv.z = p1.y; vv.w = p1.w;
-        fc_u32x2* ip = reinterpret_cast<fc_u32x2*>(a.idx + slot + t);
-        fc_u32x4* vp = reinterpret_cast<fc_u32x4*>(a.val + slot + t);
+        FC_G fc_u32x2* ip = (FC_G fc_u32x2*)(a.idx + slot + t);
+        FC_G fc_u32x4* vp = (FC_G fc_u32x4*)(a.val + slot + t);
         if (NTS) {
           __builtin_nontemporal_store(iv, ip);
           __builtin_nontemporal_store(vv, vp);
@@ -789,7 +812,7 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
     if (p < nj) {
       if (BIN) atomicAdd(&a.chist[sh.cstb[tid]], 1u);
       if (!c_ovf) {
-        uint64_t* cp = &a.cand[(uint64_t)chunk * kCandSlot + pre + p];
+        FC_G uint64_t* cp = &a.cand[(uint64_t)chunk * kCandSlot + pre + p];
         if (NTS) __builtin_nontemporal_store(sh.cst[tid], cp);
         else *cp = sh.cst[tid];
       }
@@ -832,16 +855,23 @@ __device__ __forceinline__ TopkState* mag_S(const CompactArgs& a0, uint32_t clie
 __device__ __forceinline__ MagOut mag_out(const CompactArgs& a0, uint32_t client) {
   MagOut o;
   const WsPtrs W = a0.jobs ? ws_shift(a0.W, (uint64_t)client * a0.ws_stride) : a0.W;
-  o.g = a0.g; o.idx = a0.idx; o.val = a0.val; o.cnt = a0.cnt; o.qoff = a0.qoff;
-  o.dense = a0.jobs ? nullptr : a0.dense;
+  const float* g = a0.g;
+  uint16_t* idx = a0.idx;
+  float* val = a0.val;
+  uint32_t* cnt = a0.cnt;
+  uint64_t* qoff = a0.qoff;
   if (a0.jobs) {                                // {g, idx, val, cnt} = first 32 B of the job
     const fc_u32x8 v = sload8(&a0.jobs[client]);
-    o.g = as_ptr<const float>(v[0], v[1]); o.idx = as_ptr<uint16_t>(v[2], v[3]);
-    o.val = as_ptr<float>(v[4], v[5]); o.cnt = as_ptr<uint32_t>(v[6], v[7]);
+    g = as_ptr<const float>(v[0], v[1]); idx = as_ptr<uint16_t>(v[2], v[3]);
+    val = as_ptr<float>(v[4], v[5]); cnt = as_ptr<uint32_t>(v[6], v[7]);
     const fc_u32x2 qv = sload2(&a0.jobs[client].qoff);
-    o.qoff = as_ptr<uint64_t>(qv.x, qv.y);
+    qoff = as_ptr<uint64_t>(qv.x, qv.y);
   }
-  o.S = W.st; o.ccnt = W.ccnt; o.cand = W.cand; o.chist = W.chist; o.ib = a0.ib;
+  o.g = (const FC_G float*)g; o.idx = (FC_G uint16_t*)idx; o.val = (FC_G float*)val;
+  o.cnt = (FC_G uint32_t*)cnt; o.qoff = (FC_G uint64_t*)qoff;
+  o.dense = (FC_G float*)(a0.jobs ? nullptr : a0.dense);
+  o.S = W.st; o.ccnt = (FC_G uint32_t*)W.ccnt; o.cand = (FC_G uint64_t*)W.cand; o.chist = W.chist;
+  o.ib = a0.ib;
   return o;
 }
 
@@ -936,13 +966,22 @@ __device__ __forceinline__ void compact_mag_item(const CompactArgs& a0, const Ma
 #ifndef FC_MAG1_IL
 #define FC_MAG1_IL 64
 #endif
-// Dispatch order: workgroups are dispatched x-fastest, so the linear id L = y*nch + x is
-// re-mapped to interleave the chunks of FC_MAG1_IL clients (chunk-major within a group of
-// clients): FC_MAG1_IL address streams are in flight at once instead of one.  Measured
-// (tools/kbench.py --batch 64, 128 M floats): IL 1 / 4 / 8 / 32 / 64 = 8.49 / 7.98 / 7.97 /
-// 7.58 / 7.57 ms per 64-client launch.  Not the candidate-histogram atomics (dropping them
-// changes nothing) and not address diversity (rotating each client's start chunk: 7.76 ms).
-__device__ __forceinline__ void mag_item_of(uint32_t& client, uint32_t& chunk) {
+// Dispatch order: workgroups are dispatched x-fastest, so the chunks of FC_MAG1_IL clients are
+// interleaved (chunk-major within a group of clients): FC_MAG1_IL address streams are in
+// flight at once instead of one.  Measured (tools/kbench.py --batch 64, 128 M floats): IL 1 / 4
+// / 8 / 32 / 64 = 8.49 / 7.98 / 7.97 / 7.58 / 7.57 ms per 64-client launch.  Not the
+// candidate-histogram atomics (dropping them changes nothing) and not address diversity
+// (rotating each client's start chunk: 7.76 ms).  The grid says it directly (grid3: x = client
+// in the group, y = chunk, z = group); a linear grid re-mapped with two integer divisions at
+// every workgroup's start (~60 scalar instructions ahead of the first load) took 1.2 % longer
+// at 64 x 128 M (profiles/r05_ab_compact_grid3d.jsonl) and is kept for > 65535 chunks (the
+// grid's y limit).
+__device__ __forceinline__ void mag_item_of(const CompactArgs& a0, uint32_t& client, uint32_t& chunk) {
+  if (a0.grid3) {
+    client = blockIdx.z * gridDim.x + blockIdx.x;
+    chunk = blockIdx.y;
+    return;
+  }
   if (FC_MAG1_IL == 1) {
     client = blockIdx.y; chunk = blockIdx.x;
     return;
@@ -961,7 +1000,8 @@ template <int NW, bool DENSE = false, bool NTS = false>
 __device__ __forceinline__ void compact_mag_wg(const CompactArgs& a0) {
   __shared__ __attribute__((aligned(16))) MagShared sh;
   uint32_t client, chunk;
-  mag_item_of(client, chunk);
+  mag_item_of(a0, client, chunk);
+  if (client >= a0.m) return;                            // a partial last group
   float x[MagGeo<NW>::kQ];
   mag_load<NW>(mag_g(a0, client), chunk, a0.n, x);       // g first, state behind it
   const MagState st = mag_state(mag_S(a0, client));
