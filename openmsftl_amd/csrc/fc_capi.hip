@@ -208,10 +208,15 @@ static int launch_sample(int key_mode, dim3 grid, const float* g, const SamplePl
                          fc_packet_hdr* hdr, const HdrInit& hi, const fc_encode_job* jobs,
                          uint64_t stride, hipStream_t s) {
   TimedLaunch t(FC_TIME_SAMPLE, s);
-  if (key_mode == FC_KEY_PHILOX)
+  if (key_mode == FC_KEY_PHILOX) {
     hipLaunchKernelGGL(k_sample1<kKeyPhilox>, grid, dim3(kBlock), 0, s, g, P, seed, offset, W, ib, hdr, hi, jobs, stride);
-  else
+  } else if (jobs) {                 // batched: one pilot per client, then the sample
+    hipLaunchKernelGGL(k_pilot<kKeyMag>, dim3(grid.y), dim3(kBlock), 0, s, P, W, jobs, stride);
+    FC_LAUNCHED("k_pilot");
+    hipLaunchKernelGGL((k_sample1<kKeyMag, true>), grid, dim3(kBlock), 0, s, g, P, seed, offset, W, ib, hdr, hi, jobs, stride);
+  } else {
     hipLaunchKernelGGL(k_sample1<kKeyMag>, grid, dim3(kBlock), 0, s, g, P, seed, offset, W, ib, hdr, hi, jobs, stride);
+  }
   FC_LAUNCHED("k_sample1");
   return FC_OK;
 }

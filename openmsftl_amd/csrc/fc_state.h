@@ -17,7 +17,8 @@ struct alignas(16) TopkState {
   uint32_t err;          // sticky device error (spin timeout)
   uint32_t a_done, b_done, r_done;
   uint32_t pad0_[3];
-  uint32_t win_flag;     // (unused: k_fused_mag's window flags live in WsPtrs::pub)
+  uint32_t win_flag;     // batched encode: k_pilot's fine window for k_sample1 (bit 31 valid,
+                         // level-1 bins hi << 12 | lo; k_fused_mag's live in WsPtrs::pub)
   uint32_t pad1_[2];
   uint32_t t_lo, t_hi;   // bracket (keys): list key >= t_lo; candidates key <= t_hi
   uint32_t sbin;         // candidate histogram bin = (key - t_lo) >> sbin  (< 4096 bins)

@@ -308,7 +308,7 @@ struct SampleShared {
 // records of W.pub, tag pub | bit 31).
 // SHARED_ONLY: the launch is a lone client's (the window always comes from workgroup 0's own
 // segments): no second set of pilot registers (k_fused_mag runs in 64 VGPRs)
-template <int KM, bool SHARED_ONLY = false, typename T = float>
+template <int KM, bool SHARED_ONLY = false, typename T = float, bool PRE = false>
 __device__ __forceinline__ void sample_body(const T* __restrict__ g, const SamplePlan& P,
                                             uint64_t seed, uint64_t off, const WsPtrs& W,
                                             uint32_t ib, fc_packet_hdr* hdr, const HdrInit& HI,
@@ -346,7 +346,12 @@ __device__ __forceinline__ void sample_body(const T* __restrict__ g, const Sampl
   for (int b = tid; b < kHistBins; b += kBlock) h[b] = 0;
   FineWin F;
   if (SHARED_ONLY) shared_pilot = true;
-  if (!shared_pilot || bid == 0) {
+  if (PRE) {
+    // a batched launch: k_pilot (the previous launch) left this client's window in win_flag
+    const uint32_t w = S->win_flag;
+    F = win_of(w & 0xfffu, (w >> 12) & 0xfffu);
+    if ((w >> 31) == 0u) { F.klo = 0; F.khi = 0xffffffffu; F.fs = 31; }   // (never expected)
+  } else if (!shared_pilot || bid == 0) {
     F = pilot_window<KM, SHARED_ONLY, T>(g, P, seed, off, h, s_tmp, s_out, bid == 0, xs, es, ls);
     // publish the window as ONE sc1 word (its two level-1 bins, bit 31 = valid): the pollers'
     // load returns the payload itself (a flag then three payload loads was one more round trip);
@@ -372,19 +377,50 @@ __device__ __forceinline__ void sample_body(const T* __restrict__ g, const Sampl
   __syncthreads();
   FC_TR(2);
   // ---- this workgroup's share of the sample ----
-  for (uint32_t v = bid;;) {
+  // (Binning one below-window key in four, the rest exactly, changed nothing: the batched
+  // sample's ~20 us of group loads + binning run at ~6.4 TB/s of sample bytes, FC_TRACE,
+  // profiles/r05_ab_sample_pilot_sub4.jsonl.)
+  auto hist_group = [&](const float4 (&xg)[kSampleSegs], const uint32_t (&eg)[kSampleSegs],
+                        const uint32_t (&lg)[kSampleSegs]) {
 #pragma unroll
     for (int q = 0; q < kSampleSegs; ++q) {
-      if (es[q] < ls[q]) {
-        const uint4 kk = keys4<KM>(xs[q], es[q], seed, off);
+      if (eg[q] < lg[q]) {
+        const uint4 kk = keys4<KM>(xg[q], eg[q], seed, off);
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          if (es[q] + j < ls[q]) atomicAdd(&h[fine_bin(u4get(kk, j), F)], 1u);
+          if (eg[q] + j < lg[q]) atomicAdd(&h[fine_bin(u4get(kk, j), F)], 1u);
       }
     }
-    v += nb;
-    if (SHARED_ONLY || v >= P.pstride) break;    // (k_fused_mag: one group per workgroup)
-    load_group(v);
+  };
+  if (PRE) {
+    // no pilot registers: the next group's loads are in flight while this one is binned
+    for (uint32_t v = bid;;) {
+      const uint32_t vn = v + nb;
+      float4 xn[kSampleSegs];
+      uint32_t en[kSampleSegs], ln[kSampleSegs];
+#pragma unroll
+      for (int q = 0; q < kSampleSegs; ++q) {
+        const uint32_t s = vn + (uint32_t)q * P.pstride;
+        en[q] = ln[q] = 0;
+        xn[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (vn < P.pstride && s < P.nseg) {
+          seg_lane(P, s, tid, en[q], ln[q]);
+          if (en[q] < ln[q]) xn[q] = load4_sample(g, en[q], ln[q]);
+        }
+      }
+      hist_group(xs, es, ls);
+      if (vn >= P.pstride) break;
+#pragma unroll
+      for (int q = 0; q < kSampleSegs; ++q) { xs[q] = xn[q]; es[q] = en[q]; ls[q] = ln[q]; }
+      v = vn;
+    }
+  } else {
+    for (uint32_t v = bid;;) {
+      hist_group(xs, es, ls);
+      v += nb;
+      if (SHARED_ONLY || v >= P.pstride) break;  // (k_fused_mag: one group per workgroup)
+      load_group(v);
+    }
   }
   __syncthreads();
   FC_TR(3);
@@ -455,7 +491,31 @@ __device__ __forceinline__ void sample_body(const T* __restrict__ g, const Sampl
   FC_TR(6);
 }
 
+// k_pilot: a batched encode's fine windows, one workgroup per client (grid = clients): the
+// pilot's level-1 histogram and ranks (pilot_window) once per client, left in the client's
+// win_flag for k_sample1<KM, true> (the next launch).  Every batched k_sample1 workgroup used
+// to compute its client's window itself: 16 x 128 copies of the same pilot at configs[2], each
+// 4096 conflicting LDS atomics and a rank search (~9 us of each workgroup's ~50 us chain,
+// FC_TRACE, profiles/r05_trace_batch_16M.json).
 template <int KM>
+__global__ __launch_bounds__(kBlock) void k_pilot(SamplePlan P, WsPtrs W, const fc_encode_job* jobs,
+                                                  uint64_t ws_stride) {
+  __shared__ uint32_t h[kHistBins];
+  __shared__ uint32_t s_tmp[8], s_out[4];
+  const fc_encode_job& J = jobs[blockIdx.x];
+  const float* g = J.g;
+  W = ws_shift(W, (uint64_t)blockIdx.x * ws_stride);
+  for (int b = threadIdx.x; b < kHistBins; b += kBlock) h[b] = 0;
+  float4 xs[kSampleSegs];
+  uint32_t es[kSampleSegs], ls[kSampleSegs];
+#pragma unroll
+  for (int q = 0; q < kSampleSegs; ++q) { xs[q] = make_float4(0.f, 0.f, 0.f, 0.f); es[q] = ls[q] = 0; }
+  const FineWin F = pilot_window<KM>(g, P, J.seed, J.offset, h, s_tmp, s_out, false, xs, es, ls);
+  if (threadIdx.x == 0) W.st->win_flag = 0x80000000u | ((F.khi >> 19) << 12) | (F.klo >> 19);
+}
+template __global__ void k_pilot<kKeyMag>(SamplePlan, WsPtrs, const fc_encode_job*, uint64_t);
+
+template <int KM, bool PRE = false>
 __global__ __launch_bounds__(kBlock, 8) void k_sample1(const float* __restrict__ g, SamplePlan P,
                                                     uint64_t seed, uint64_t off, WsPtrs W,
                                                     uint32_t ib, fc_packet_hdr* hdr, HdrInit HI,
@@ -468,9 +528,10 @@ __global__ __launch_bounds__(kBlock, 8) void k_sample1(const float* __restrict__
     HI.seed = seed; HI.offset = off;
     W = ws_shift(W, (uint64_t)blockIdx.y * ws_stride);
   }
-  // every workgroup computes the pilot window itself (no workgroup of this launch waits for
-  // another: safe beside any other kernel); only k_fused_mag shares workgroup 0's window
-  sample_body<KM>(g, P, seed, off, W, ib, hdr, HI, blockIdx.x, gridDim.x, false, sm, 0u);
+  // every workgroup computes the pilot window itself, or (PRE: batched) reads the one k_pilot
+  // left (no workgroup of this launch waits for another: safe beside any other kernel); only
+  // k_fused_mag shares workgroup 0's window
+  sample_body<KM, false, float, PRE>(g, P, seed, off, W, ib, hdr, HI, blockIdx.x, gridDim.x, false, sm, 0u);
 }
 
 
@@ -1527,7 +1588,8 @@ __global__ __launch_bounds__(kBlock) void k_engine(EngineArgs a) {
 // --------------------------------------------------------------------------------------
 // explicit instantiations used by fc_capi.hip
 // --------------------------------------------------------------------------------------
-template __global__ void k_sample1<kKeyMag>(const float*, SamplePlan, uint64_t, uint64_t, WsPtrs, uint32_t, fc_packet_hdr*, HdrInit, const fc_encode_job*, uint64_t);
+template __global__ void k_sample1<kKeyMag, false>(const float*, SamplePlan, uint64_t, uint64_t, WsPtrs, uint32_t, fc_packet_hdr*, HdrInit, const fc_encode_job*, uint64_t);
+template __global__ void k_sample1<kKeyMag, true>(const float*, SamplePlan, uint64_t, uint64_t, WsPtrs, uint32_t, fc_packet_hdr*, HdrInit, const fc_encode_job*, uint64_t);
 template __global__ void k_engine<kKeyMag>(EngineArgs);
 template __global__ void k_engine<kKeyPhilox>(EngineArgs);
 
