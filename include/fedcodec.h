@@ -28,10 +28,12 @@
  * Concurrency: every entry point may run beside any other kernel, on any stream, with one
  * exception.  fc_topk_encode (key_mode MAGNITUDE, 0 < k < n) and fc_topk_encode_dense launch
  * k_fused_mag, whose compaction workgroups wait in-kernel (bounded) for the bracket its sample
- * workgroups publish; two such launches on two streams of one device can stall each other to
- * the bound (the call then reports FC_STATUS_RETRY_EXACT: correct after the exact re-encode,
- * but late).  Queue those two on one stream, or order them with events (the Python layer
- * does: codec._fused_encode).  The batched, mask, rand-k, float64, exact, decode and fold
+ * workgroups publish; two such launches on two streams of one device can, in principle, stall
+ * each other until that bound (~8192 polls, 2-4 ms), and the call then reports
+ * FC_STATUS_RETRY_EXACT: correct after the exact re-encode, but late (400 concurrent fused
+ * encodes on two streams at 16 M: no stall, tests/test_gpu_parity.py).  Queue those two on one
+ * stream, or order them with events, to rule it out (the Python layer does:
+ * codec._fused_encode).  The batched, mask, rand-k, float64, exact, decode and fold
  * kernels synchronise only through last-arriver tickets (no workgroup waits for another).
  */
 #ifndef FEDCODEC_H_

@@ -148,7 +148,11 @@ __device__ void bitonic_desc(uint64_t* sv, uint32_t P2) {
 // (key >> 7) & 0xfff — took 17.8 + 21.5 us per 128 M gradient.)
 // --------------------------------------------------------------------------------------
 constexpr int kSampleSegs = FC_SAMPLE_SEGS_PER_WG;
-constexpr uint32_t kSpinMax = 1u << 18;   // bounded spins (~60 ms): one that never ends is a bug
+// Bounded in-kernel polls (k_fused_mag's bracket and window waits, ~0.25 us each): a bracket
+// arrives in 14-30 us (~100 polls); 8192 polls (~2-4 ms) end a co-residency stall between two
+// fused launches on two queues with a RETRY (the exact re-encode) instead of ~60 ms
+// (tests/test_gpu_parity.py::test_fused_encodes_on_concurrent_streams_are_bounded).
+constexpr uint32_t kSpinMax = 1u << 13;
 constexpr uint32_t kFineLo = 1024, kFineBins = 2048, kFineHi = kFineLo + kFineBins;
 constexpr uint32_t kCoarseShift = 21;            // 0x7fffffff >> 21 = 1023
 

@@ -499,6 +499,54 @@ def test_batch_encodes_on_concurrent_streams_stay_ok():
     assert codec.resolve(pk) == 0
 
 
+@pytest.mark.timeout(120)
+def test_fused_encodes_on_concurrent_streams_are_bounded(monkeypatch):
+    """k_fused_mag (the lone packet and drop-in dense encodes) is the one kernel whose
+    workgroups wait in-kernel, for the bracket of their own launch.  codec orders fused encodes
+    per device; a C caller on two streams need not.  Here two of them (a packet encode and a
+    dense one, their own workspaces) run on two streams with nothing ordering them: a
+    co-residency stall ends at the bounded poll (~2 ms) with RETRY and the exact re-encode
+    restores the result, so the loop finishes and both results equal the ordered encodes'."""
+    import contextlib
+    codec = _codec()
+    monkeypatch.setattr(codec, "_fused_encode", lambda dev: contextlib.nullcontext())
+    n, f = 1 << 24, 0.1
+    gen = torch.Generator(device="cuda").manual_seed(17)
+    g0 = torch.randn(n, device="cuda", generator=gen) * 1e-3
+    g1 = torch.randn(n, device="cuda", generator=gen) * 3e-2
+    k = co.effective_k(co.num_kept(f, n), n)
+    ref0 = _packet_bytes(codec.encode_top(g0, k))
+    ref1 = codec.decode(codec.encode_top(g1, k)).clone()
+    s0, s1 = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s0):
+        p0 = codec.encode_top(g0, k, check=False)
+    with torch.cuda.stream(s1):
+        p1 = codec.Packet.alloc(n, codec.L.FC_FMT_IDXVAL, g1.device, k=k)
+        out1 = torch.empty_like(g1)
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s0):
+        bad0 = torch.zeros((), dtype=torch.int64, device="cuda")
+    with torch.cuda.stream(s1):
+        bad1 = torch.zeros((), dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    for _ in range(200):                        # statuses counted on each stream, no host sync
+        with torch.cuda.stream(s0):
+            codec.encode_top(g0, k, packet=p0, check=False)
+            bad0 += (p0.hdr[36:40] != 0).any().to(torch.int64)
+        with torch.cuda.stream(s1):
+            codec.compress_top_dense(g1, k, out=out1, packet=p1, check=False)
+            bad1 += (p1.hdr[36:40] != 0).any().to(torch.int64)
+    torch.cuda.synchronize()
+    retries = int(bad0) + int(bad1)
+    if codec.resolve([p1]):                   # the dense call's exact re-encode
+        codec.decode(p1, out=out1)
+    codec.resolve([p0])
+    assert _packet_bytes(p0) == ref0
+    assert torch.equal(out1.view(torch.int32), ref1.view(torch.int32))
+    print(f"encodes that stalled to the poll bound (RETRY, re-encoded): {retries} of 400")
+
+
 @pytest.mark.parametrize("M,streams", [(5, 2), (7, 3), (2, 2), (1, 2)])
 def test_encode_fold_batch_pipelined(M, streams):
     """encode_fold_batch (each sub-batch folded on its stream as soon as it is encoded, the
