@@ -878,15 +878,10 @@ int fc_topk_dense_f64_sampled(const double* g, uint64_t n, uint64_t k, double* o
   a.out = out; a.status = status;
   const uint32_t rgrid = (a.nchunks + a.per - 1) / a.per;
   {
-    TimedLaunch t(FC_TIME_SAMPLE, s);
-    hipLaunchKernelGGL(k_sample64, dim3((P.nseg + kSampleSegs - 1) / kSampleSegs), dim3(kBlock),
-                       0, s, g, P, W, ib, hdr, hi);
-    FC_LAUNCHED("k_sample64");
-  }
-  {
     TimedLaunch t(FC_TIME_COMPACT, s);
-    hipLaunchKernelGGL(k_compact64, dim3(a.nchunks), dim3(kBlock), 0, s, a);
-    FC_LAUNCHED("k_compact64");
+    const uint32_t nsamp = (P.nseg + kSampleSegs - 1) / kSampleSegs;
+    hipLaunchKernelGGL(k_fused64, dim3(nsamp + a.nchunks), dim3(kBlock), 0, s, a, P, W, ib, hdr, hi, nsamp);
+    FC_LAUNCHED("k_fused64");
   }
   {
     TimedLaunch t(FC_TIME_ENGINE, s);

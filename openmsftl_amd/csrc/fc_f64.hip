@@ -278,11 +278,12 @@ __global__ __launch_bounds__(kBlock) void k_div_scalar64(double* x, uint64_t n, 
 // Sampled fast path for magnitude keys (fc_topk_dense_f64_sampled): the fp32 design on the
 // 31-bit HIGH key hk(x) = (|x| bits) >> 32 of each double (exponent + 20 mantissa bits;
 // key32 = mag_key of it, a non-decreasing map of the 95-bit comp = key64 << 32 | idx):
-//   k_sample64    k_sample1's stratified sample + pilot window over hk (sample_body<double>):
-//                 bracket [t_lo, t_hi] of key32 around the k-th key (one launch)
-//   k_compact64   ONE streaming pass, 8N read + 8N written: q = key32 >= t_lo ? g : +0;
-//                 definite (key32 > t_hi) and candidate counts into the sharded totals; each
-//                 candidate's exact comp into its chunk's slot, its bin into the histogram
+//   k_fused64     ONE launch: its first workgroups run k_sample1's stratified sample + pilot
+//                 window over hk (sample_body<double>) -> bracket [t_lo, t_hi] of key32 around
+//                 the k-th key, published to the others; each of those is a chunk of ONE
+//                 streaming pass, 8N read + 8N written: q = key32 >= t_lo ? g : +0; definite
+//                 (key32 > t_hi) and candidate counts into the sharded totals; each candidate's
+//                 exact comp into its chunk's slot, its bin into the histogram
 //   k_resolve64   rank r = k - #definite among the candidates: every workgroup finds the bin
 //                 beta holding it (the histogram, from L2) and gathers its chunks' candidates
 //                 in beta (a chunk whose candidates overflowed its slot is rescanned from
@@ -302,14 +303,6 @@ static_assert(kC64Slot * sizeof(u128) == kCandSlot * sizeof(uint64_t), "candidat
 
 __device__ __forceinline__ uint32_t key32_of(double x) { return mag_key(hikey_f(x)); }
 
-__global__ __launch_bounds__(kBlock, 8) void k_sample64(const double* __restrict__ g, SamplePlan P,
-                                                     WsPtrs W, uint32_t ib, fc_packet_hdr* hdr,
-                                                     HdrInit HI) {
-  __shared__ SampleShared sm;
-  sample_body<kKeyMag, false, double>(g, P, 0ull, 0ull, W, ib, hdr, HI, blockIdx.x, gridDim.x,
-                                      false, sm, 0u);   // every workgroup its own window: no wait
-}
-
 struct Fast64Args {
   const double* g;
   uint64_t n, k;
@@ -325,36 +318,47 @@ struct Fast64Args {
   uint32_t* status;            // caller's device word: FC_STATUS_OK / RETRY_EXACT
 };
 
-typedef double fc_d2v __attribute__((ext_vector_type(2)));
-typedef __attribute__((address_space(1))) const fc_d2v fc_gd2v;
+#ifndef FC_F64_DELAY
+#define FC_F64_DELAY 90               // k_fused64's first-round chunks: s_sleep before loading
+#endif
 
 // One workgroup per 8192-element chunk: 16 double2 per thread, coalesced (element
 // base + 2 (i * 256 + tid) + {0, 1}).
-__global__ __launch_bounds__(kBlock) void k_compact64(Fast64Args a) {
-  __shared__ uint32_t s_cnt, s_red[kBlock / 64];
-  const uint32_t chunk = blockIdx.x, tid = threadIdx.x;
+constexpr int kI64 = kChunk / (2 * kBlock);     // 16
+__device__ __forceinline__ void load64_chunk(const Fast64Args& a, uint32_t chunk, fc_d2v (&x)[kI64]) {
+  const uint32_t tid = threadIdx.x;
   const uint64_t base = (uint64_t)chunk * kChunk;
-  const bool full = base + kChunk <= a.n;
-  constexpr int kI = kChunk / (2 * kBlock);     // 16
-  fc_d2v x[kI];
-  if (full) {
+  if (base + kChunk <= a.n) {
     fc_gd2v* gp = (fc_gd2v*)(a.g + base) + tid;
 #pragma unroll
-    for (int i = 0; i < kI; ++i) x[i] = __builtin_nontemporal_load(gp + i * kBlock);
+    for (int i = 0; i < kI64; ++i) x[i] = __builtin_nontemporal_load(gp + i * kBlock);
   } else {
 #pragma unroll
-    for (int i = 0; i < kI; ++i) {
+    for (int i = 0; i < kI64; ++i) {
       const uint64_t e = base + 2ull * (i * kBlock + tid);
       x[i].x = e < a.n ? a.g[e] : 0.0;
       x[i].y = e + 1 < a.n ? a.g[e + 1] : 0.0;
     }
   }
-  if (tid == 0) s_cnt = 0;
-  const uint32_t t_lo = a.S->t_lo, t_hi = a.S->t_hi, sbin = a.S->sbin;
+}
+
+struct Compact64Shared {
+  uint32_t cnt, red[kBlock / 64];
+};
+
+// q = key32 >= t_lo ? g : +0 for one loaded chunk; candidates to the chunk's slot and the
+// histogram; the chunk's totals into the shards
+__device__ __forceinline__ void compact64_body(const Fast64Args& a, uint32_t chunk,
+                                               const fc_d2v (&x)[kI64], uint32_t t_lo,
+                                               uint32_t t_hi, uint32_t sbin, Compact64Shared& sh) {
+  const uint32_t tid = threadIdx.x;
+  const uint64_t base = (uint64_t)chunk * kChunk;
+  const bool full = base + kChunk <= a.n;
+  if (tid == 0) sh.cnt = 0;
   lds_barrier();
   uint32_t listed = 0;
 #pragma unroll
-  for (int i = 0; i < kI; ++i) {
+  for (int i = 0; i < kI64; ++i) {
     fc_d2v q;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -365,7 +369,7 @@ __global__ __launch_bounds__(kBlock) void k_compact64(Fast64Args a) {
       listed += L ? 1u : 0u;
       if (h) q.y = L ? v : 0.0; else q.x = L ? v : 0.0;
       if (L && key <= t_hi) {
-        const uint32_t pos = atomicAdd(&s_cnt, 1u);
+        const uint32_t pos = atomicAdd(&sh.cnt, 1u);
         if (pos < (uint32_t)kC64Slot) {
           const uint64_t key64 = mag_key64(v);
           uint64_t* d = reinterpret_cast<uint64_t*>(&a.cand[(uint64_t)chunk * kC64Slot + pos]);
@@ -384,17 +388,60 @@ __global__ __launch_bounds__(kBlock) void k_compact64(Fast64Args a) {
     }
   }
   listed = wave_sum(listed);
-  if ((tid & 63) == 0) s_red[tid >> 6] = listed;
+  if ((tid & 63) == 0) sh.red[tid >> 6] = listed;
   __syncthreads();
   if (tid == 0) {
     uint32_t tot = 0;
 #pragma unroll
-    for (int w = 0; w < kBlock / 64; ++w) tot += s_red[w];
+    for (int w = 0; w < kBlock / 64; ++w) tot += sh.red[w];
     if (chunk == 0) *a.status = (uint32_t)FC_STATUS_OK;   // this call's status (k_resolve64)
-    a.ccnt[chunk] = s_cnt;
+    a.ccnt[chunk] = sh.cnt;
     atomicAdd(&a.S->shard_ent[chunk % kShards], tot);
-    if (s_cnt) atomicAdd(&a.S->shard_cnd[chunk % kShards], s_cnt);
+    if (sh.cnt) atomicAdd(&a.S->shard_cnd[chunk % kShards], sh.cnt);
   }
+}
+
+// k_fused64: k_fused_mag's form for float64 (round 5; before, k_sample64 and k_compact64 were
+// two launches): workgroups [0, nsamp) run the sample over the high keys (workgroup 0's
+// segments are the pilot, its window published in line-spread copies), every other one is a
+// chunk that issues its loads, polls its copy of the 16-B bracket record (tag fz_seq + 1,
+// bounded) and streams q.  The sample never waits for a chunk workgroup; a timed-out poll sets
+// S->err and k_resolve64 reports RETRY.
+union Fused64Shared {
+  SampleShared s;
+  Compact64Shared c;
+};
+__global__ __launch_bounds__(kBlock) void k_fused64(Fast64Args a, SamplePlan P, WsPtrs W,
+                                                    uint32_t ib, fc_packet_hdr* hdr, HdrInit HI,
+                                                    uint32_t nsamp) {
+  __shared__ Fused64Shared u;
+  __shared__ uint32_t s_b[3];
+  const uint32_t pub = sload2(&a.S->fz_seq).x + 1u;      // not written by this launch
+  if (blockIdx.x < nsamp) {
+    sample_body<kKeyMag, true, double>(a.g, P, 0ull, 0ull, W, ib, hdr, HI, blockIdx.x, nsamp,
+                                       true, u.s, pub);
+    return;
+  }
+  const uint32_t chunk = blockIdx.x - nsamp;
+  fc_d2v x[kI64];
+#if FC_F64_DELAY
+  if (chunk < 1024u) __builtin_amdgcn_s_sleep(FC_F64_DELAY);   // the sample's loads first
+#endif
+  load64_chunk(a, chunk, x);
+  if (threadIdx.x == 0) {
+    const uint32_t* rec = &W.pub[(blockIdx.x % kPubCopies) * kPubStride];
+    const uint32_t tag = pub | 0x80000000u;
+    uint32_t it = 0;
+    fc_rec4 r = ld16_agent(rec);
+    while (r.w != tag && ++it < kSpinMax) {
+      __builtin_amdgcn_s_sleep(4);
+      r = ld16_agent(rec);
+    }
+    if (it >= kSpinMax) st_agent(&a.S->err, 1u);
+    s_b[0] = r.x; s_b[1] = r.y; s_b[2] = r.z;
+  }
+  __syncthreads();
+  compact64_body(a, chunk, x, s_b[0], s_b[1], s_b[2], u.c);
 }
 
 // fn(comp) for every candidate of this workgroup's chunk range: kTpc64 threads per chunk read
@@ -512,7 +559,8 @@ __global__ __launch_bounds__(kBlock) void k_resolve64(Fast64Args a) {
     const uint32_t st = retry ? (uint32_t)FC_STATUS_RETRY_EXACT : (uint32_t)FC_STATUS_OK;
     a.E->small_n = 0;
     S->err = 0;
-    atomicMax(a.status, st);                              // (k_compact64 reset it to OK)
+    S->fz_seq += 1u;                                      // k_fused64: the next launch's tag
+    atomicMax(a.status, st);                              // (k_fused64 reset it to OK)
   }
 }
 
