@@ -1082,3 +1082,25 @@ def test_flat_stage_arguments():
         FlatLayout([torch.zeros(3, dtype=torch.float64, device="cuda")])
     with pytest.raises(ValueError):
         FlatLayout([])
+
+
+@pytest.mark.timeout(120)
+def test_batched_compaction_past_the_grid_y_limit():
+    """k_compact_mag1 runs on a 3-D grid (client in the interleave group, chunk, group) while a
+    client has at most 65,535 chunks (the grid's y limit) and on the linear, divided grid past
+    it.  One gradient of 2^29 + 12,345 elements (65,537 chunks) through the batched encode
+    (linear grid) and through the lone fused encode (k_fused_mag, which maps chunks itself): the
+    two packets are byte-equal (same plan, same bracket), and the decoded result keeps exactly k
+    coordinates, none smaller in magnitude than any dropped one."""
+    codec = _codec()
+    n, f = (1 << 29) + 12_345, 0.01
+    g = torch.randn(n, device="cuda", generator=torch.Generator(device="cuda").manual_seed(23))
+    k = co.effective_k(co.num_kept(f, n), n)
+    lone = codec.encode_top(g, k)
+    [batch] = codec.encode_top_batch([g], k)
+    torch.cuda.synchronize()
+    assert _packet_bytes(batch) == _packet_bytes(lone)
+    q = codec.decode(batch)
+    kept = q != 0
+    assert int(kept.sum()) == k
+    assert float(g.abs()[kept].min()) >= float(g.abs()[~kept].max())
