@@ -549,15 +549,43 @@ def single_gradient(torch, codec, g, k, n, iters=20):
     moved = dense_moved_bytes(n, pkt)
     codec.resolve([pkt])
     alg = 8.0 * n + 2 * ENTRY_BYTES * k
+    # the same calls, `iters` of them captured in one HIP graph (codec.GraphedCalls) and
+    # replayed: no host work per call, cheaper kernel boundaries; same kernels, same buffers
+    dt_g = _graph_us(torch, codec, lambda: (codec.encode_top(g, k, packet=pkt, check=False),
+                                            codec.decode(pkt, out=out)), iters) * 1e-6
+    codec.resolve([pkt])
+    dt_dg = _graph_us(torch, codec, lambda: codec.compress_top_dense(g, k, out=out, packet=pkt,
+                                                                     check=False), iters) * 1e-6
+    codec.resolve([pkt])
     return {"n": n, "k": k, "us_per_encode_decode": round(dt * 1e6, 1),
             "grad_GBps": round(4.0 * n / dt / 1e9, 1),
             "alg_GBps": round(alg / dt / 1e9, 1),
             "hbm_frac": round(alg / dt / 1e9 / HBM_PEAK_GBPS, 4),
+            "graph": {"us_per_encode_decode": round(dt_g * 1e6, 1),
+                      "hbm_frac": round(alg / dt_g / 1e9 / HBM_PEAK_GBPS, 4)},
             "fused_dense": {"us": round(dt_d * 1e6, 1),
                             "alg_GBps": round(alg / dt_d / 1e9, 1),
                             "hbm_frac": round(alg / dt_d / 1e9 / HBM_PEAK_GBPS, 4),
                             "moved_bytes": int(moved),
-                            "hbm_frac_moved": round(moved / dt_d / 1e9 / HBM_PEAK_GBPS, 4)}}
+                            "hbm_frac_moved": round(moved / dt_d / 1e9 / HBM_PEAK_GBPS, 4),
+                            "graph": {"us": round(dt_dg * 1e6, 1),
+                                      "hbm_frac": round(alg / dt_dg / 1e9 / HBM_PEAK_GBPS, 4),
+                                      "hbm_frac_moved": round(moved / dt_dg / 1e9 / HBM_PEAK_GBPS, 4)}}}
+
+
+def _graph_us(torch, codec, fn, iters=20, reps=3):
+    """Per-call µs of `iters` calls of fn captured in one HIP graph, best of `reps` replays."""
+    gc = codec.GraphedCalls(lambda: [fn() for _ in range(iters)])
+    best = None
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        gc.replay()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / iters * 1e6
+        best = dt if best is None else min(best, dt)
+    del gc
+    return best
 
 
 def dense_moved_bytes(n, pkt):

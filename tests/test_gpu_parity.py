@@ -1104,3 +1104,50 @@ def test_batched_compaction_past_the_grid_y_limit():
     kept = q != 0
     assert int(kept.sum()) == k
     assert float(g.abs()[kept].min()) >= float(g.abs()[~kept].max())
+
+
+@pytest.mark.timeout(120)
+def test_graphed_calls_equal_eager_calls():
+    """codec.GraphedCalls: the lone packet encode + decode, the drop-in dense encode and a
+    batched encode + fold, captured into one HIP graph and replayed three times, give the eager
+    calls' bytes (the fused kernels' bracket tags and every self-cleaning counter live on the
+    device, so replays line up with eager calls)."""
+    codec = _codec()
+    from openmsftl_amd import _lib as L
+    n, M, f = 3_000_017, 6, 0.1
+    dev = torch.device("cuda", 0)
+    gen = torch.Generator(device="cuda").manual_seed(29)
+    grads = [torch.randn(n, device="cuda", generator=gen) * (10.0 ** -(1 + i % 3)) for i in range(M)]
+    k = co.effective_k(co.num_kept(f, n), n)
+    ref_pkt = _packet_bytes(codec.encode_top(grads[0], k))
+    ref_dense = codec.compress_top_dense(grads[1], k).clone()
+    w = [1.0 / M] * M
+    ref_pk = codec.encode_top_batch(grads, k)
+    ref_acc = codec.decode_accumulate(ref_pk, w).clone()
+    pkt = codec.Packet.alloc(n, L.FC_FMT_IDXVAL, dev, k=k)
+    out = torch.empty(n, dtype=torch.float32, device=dev)
+    dpkt = codec.Packet.alloc(n, L.FC_FMT_IDXVAL, dev, k=k)
+    dense = torch.empty(n, dtype=torch.float32, device=dev)
+    pk = [codec.Packet.alloc(n, L.FC_FMT_IDXVAL, dev, k=k) for _ in range(M)]
+    jobs = codec.encode_jobs(grads, pk)
+    views = codec.views_tensor(pk, w, dev)
+    acc = torch.empty(n, dtype=torch.float32, device=dev)
+
+    def calls():
+        codec.encode_top(grads[0], k, packet=pkt, check=False)
+        codec.decode(pkt, out=out)
+        codec.compress_top_dense(grads[1], k, out=dense, packet=dpkt, check=False)
+        codec.encode_top_batch(grads, k, packets=pk, jobs=jobs, check=False)
+        codec.decode_accumulate(pk, w, out=acc, views=views)
+
+    gc = codec.GraphedCalls(calls)
+    for _ in range(3):
+        out.zero_(); dense.zero_(); acc.zero_()
+        gc.replay()
+        torch.cuda.synchronize()
+        assert codec.resolve([pkt]) == 0 and codec.resolve(pk) == 0
+        assert dpkt.header().status == 0
+        assert _packet_bytes(pkt) == ref_pkt
+        assert torch.equal(dense.view(torch.int32), ref_dense.view(torch.int32))
+        assert torch.equal(acc.view(torch.int32), ref_acc.view(torch.int32))
+        assert torch.equal(out.view(torch.int32), codec.decode(codec.encode_top(grads[0], k)).view(torch.int32))
