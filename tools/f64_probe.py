@@ -1,5 +1,5 @@
 """float64 top-k on one gradient (fc_topk_dense_f64_sampled): HIP-event averages per launch
-class (k_sample64 = SAMPLE, k_compact64 = COMPACT, k_resolve64 (+ k_fixup64) = ENGINE), wall
+class (k_fused64 = COMPACT: the sample and the streaming pass in one launch; k_resolve64 = ENGINE), wall
 time per call, and the exact engine for comparison.
 
     python tools/f64_probe.py [--lib tools/variants/lib_X.so] [--n 16777216] [--f 0.1]
