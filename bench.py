@@ -480,7 +480,7 @@ def main():
     extra["process_group"] = ({"backend": args.backend, "world": world,
                                "collective_per_step": "reduce (async)"} if pg else None)
     if rank == 0 and not args.no_single:
-        extra["single_gradient"] = single_gradient(torch, codec, grads[0], k, n)
+        extra["single_gradient"] = single_gradient(torch, codec, grads[0], k, n, graph=not pg)
         extra["qsgd_single_gradient"] = qsgd_single(torch, codec, grads[0], n)
 
     # the other named single-GPU sizes (BASELINE configs[1], configs[2]) as extras, after the
@@ -488,7 +488,7 @@ def main():
     del grads, pkts, jobs, views, fold, hdrs
     torch.cuda.empty_cache()
     if world == 1 and rank == 0 and not args.no_single:
-        extra["configs_1_2"] = small_configs(torch, codec, L, device, f)
+        extra["configs_1_2"] = small_configs(torch, codec, L, device, f, graph=not pg)
     if world == 1 and rank == 0 and not args.no_matrix:
         extra["codec_matrix"] = codec_matrix(torch, codec, L, device)
 
@@ -521,7 +521,7 @@ def main():
         dist.destroy_process_group()
 
 
-def single_gradient(torch, codec, g, k, n, iters=20):
+def single_gradient(torch, codec, g, k, n, iters=20, graph=True):
     """North-star probe: encode+decode of ONE 128 M gradient (packet -> dense), HBM fraction
     of the algorithmic 8N + 16k bytes."""
     out = torch.empty_like(g)
@@ -549,6 +549,17 @@ def single_gradient(torch, codec, g, k, n, iters=20):
     moved = dense_moved_bytes(n, pkt)
     codec.resolve([pkt])
     alg = 8.0 * n + 2 * ENTRY_BYTES * k
+    res = {"n": n, "k": k, "us_per_encode_decode": round(dt * 1e6, 1),
+           "grad_GBps": round(4.0 * n / dt / 1e9, 1),
+           "alg_GBps": round(alg / dt / 1e9, 1),
+           "hbm_frac": round(alg / dt / 1e9 / HBM_PEAK_GBPS, 4),
+           "fused_dense": {"us": round(dt_d * 1e6, 1),
+                           "alg_GBps": round(alg / dt_d / 1e9, 1),
+                           "hbm_frac": round(alg / dt_d / 1e9 / HBM_PEAK_GBPS, 4),
+                           "moved_bytes": int(moved),
+                           "hbm_frac_moved": round(moved / dt_d / 1e9 / HBM_PEAK_GBPS, 4)}}
+    if not graph:                      # (N > 1: no graph capture beside a live process group)
+        return res
     # the same calls, `iters` of them captured in one HIP graph (codec.GraphedCalls) and
     # replayed: no host work per call, cheaper kernel boundaries; same kernels, same buffers
     dt_g = _graph_us(torch, codec, lambda: (codec.encode_top(g, k, packet=pkt, check=False),
@@ -557,20 +568,12 @@ def single_gradient(torch, codec, g, k, n, iters=20):
     dt_dg = _graph_us(torch, codec, lambda: codec.compress_top_dense(g, k, out=out, packet=pkt,
                                                                      check=False), iters) * 1e-6
     codec.resolve([pkt])
-    return {"n": n, "k": k, "us_per_encode_decode": round(dt * 1e6, 1),
-            "grad_GBps": round(4.0 * n / dt / 1e9, 1),
-            "alg_GBps": round(alg / dt / 1e9, 1),
-            "hbm_frac": round(alg / dt / 1e9 / HBM_PEAK_GBPS, 4),
-            "graph": {"us_per_encode_decode": round(dt_g * 1e6, 1),
-                      "hbm_frac": round(alg / dt_g / 1e9 / HBM_PEAK_GBPS, 4)},
-            "fused_dense": {"us": round(dt_d * 1e6, 1),
-                            "alg_GBps": round(alg / dt_d / 1e9, 1),
-                            "hbm_frac": round(alg / dt_d / 1e9 / HBM_PEAK_GBPS, 4),
-                            "moved_bytes": int(moved),
-                            "hbm_frac_moved": round(moved / dt_d / 1e9 / HBM_PEAK_GBPS, 4),
-                            "graph": {"us": round(dt_dg * 1e6, 1),
-                                      "hbm_frac": round(alg / dt_dg / 1e9 / HBM_PEAK_GBPS, 4),
-                                      "hbm_frac_moved": round(moved / dt_dg / 1e9 / HBM_PEAK_GBPS, 4)}}}
+    res["graph"] = {"us_per_encode_decode": round(dt_g * 1e6, 1),
+                    "hbm_frac": round(alg / dt_g / 1e9 / HBM_PEAK_GBPS, 4)}
+    res["fused_dense"]["graph"] = {"us": round(dt_dg * 1e6, 1),
+                                   "hbm_frac": round(alg / dt_dg / 1e9 / HBM_PEAK_GBPS, 4),
+                                   "hbm_frac_moved": round(moved / dt_dg / 1e9 / HBM_PEAK_GBPS, 4)}
+    return res
 
 
 def _graph_us(torch, codec, fn, iters=20, reps=3):
@@ -596,13 +599,13 @@ def dense_moved_bytes(n, pkt):
     return 8.0 * n + 16.0 * pkt.header().n_cand
 
 
-def small_configs(torch, codec, L, device, f, n=16_777_216, M=128, steps=100):
+def small_configs(torch, codec, L, device, f, n=16_777_216, M=128, steps=100, graph=True):
     """BASELINE configs[1] (one 16 M gradient: encode + dense decode) and configs[2] (128
     clients x 16 M: batched encode + on-device FedAVG fold), device-resident, same codec."""
     from openmsftl_amd.compression import kept_count
     k = kept_count(f, n)
     grads = make_grads(M, n, 0, device, torch)
-    one = single_gradient(torch, codec, grads[0], k, n)
+    one = single_gradient(torch, codec, grads[0], k, n, graph=graph)
     pkts = [codec.Packet.alloc(n, L.FC_FMT_IDXVAL, device, k=k) for _ in range(M)]
     w = [1.0 / M] * M
     jobs = codec.encode_jobs(grads, pkts)

@@ -513,7 +513,9 @@ class GraphedCalls:
                 fn()
         self.stream.synchronize()
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph, stream=self.stream):
+        # thread_local: another thread's stream work (e.g. a process group's watchdog polling
+        # its events) is not an error during this capture
+        with torch.cuda.graph(self.graph, stream=self.stream, capture_error_mode="thread_local"):
             fn()
         torch.cuda.current_stream(dev).wait_stream(self.stream)
 
