@@ -145,9 +145,10 @@ static SamplePlan make_plan(uint64_t n, uint64_t k, bool single = false) {
   P.cbins_log2 = 12;                 // lone encodes (fused in-kernel binning); batched: below
   // pilot (k_sample1): kPilotSegs segments spread over the sample, read by every workgroup.
   // Its ranks bracket the sample ranks scaled to the pilot, widened by 7 pilot sigmas + 8.
-  P.pstride = (P.nseg + kSampleSegs - 1) / kSampleSegs;          // the sample grid
+  P.segs = n <= (32ull << 20) ? 2u : (uint32_t)kSampleSegs;
+  P.pstride = (P.nseg + P.segs - 1) / P.segs;                    // the sample grid
   P.np = 0;
-  while (P.np < (uint32_t)kPilotSegs && P.np * P.pstride < P.nseg) ++P.np;
+  while (P.np < P.segs && P.np * P.pstride < P.nseg) ++P.np;
   double Sp = 0.0;
   for (uint32_t j = 0; j < P.np; ++j) {
     const uint64_t st = seg_start(P, pilot_seg(P, j));
@@ -471,7 +472,7 @@ int fc_topk_encode(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
   const SamplePlan P = make_plan(n, k);
-  const uint32_t sgrid = (P.nseg + kSampleSegs - 1) / kSampleSegs;   // <= 256
+  const uint32_t sgrid = (P.nseg + P.segs - 1) / P.segs;   // <= 256
   if (key_mode == FC_KEY_MAGNITUDE && fused_enabled()) {
     rc = launch_fused(ca, P, hi, sgrid, s);
     if (rc) return rc;
@@ -506,7 +507,7 @@ int fc_topk_encode_dense(const float* g, uint64_t n, uint64_t k, uint16_t* idx, 
   }
   hipStream_t s = (hipStream_t)stream;
   const SamplePlan P = make_plan(n, k, true);
-  const uint32_t sgrid = (P.nseg + kSampleSegs - 1) / kSampleSegs;
+  const uint32_t sgrid = (P.nseg + P.segs - 1) / P.segs;
   if (fused_enabled()) {
     rc = launch_fused(ca, P, hi, sgrid, s);
     if (rc) return rc;
@@ -879,7 +880,7 @@ int fc_topk_dense_f64_sampled(const double* g, uint64_t n, uint64_t k, double* o
   const uint32_t rgrid = (a.nchunks + a.per - 1) / a.per;
   {
     TimedLaunch t(FC_TIME_COMPACT, s);
-    const uint32_t nsamp = (P.nseg + kSampleSegs - 1) / kSampleSegs;
+    const uint32_t nsamp = (P.nseg + P.segs - 1) / P.segs;
     hipLaunchKernelGGL(k_fused64, dim3(nsamp + a.nchunks), dim3(kBlock), 0, s, a, P, W, ib, hdr, hi, nsamp);
     FC_LAUNCHED("k_fused64");
   }

@@ -142,12 +142,14 @@ struct SamplePlan {
   uint32_t pstride;    // their spacing = the sample grid (segment j*pstride, j < np)
   int64_t pr_hi, pr_lo;  // pilot ranks (1-based from the top) that bound the fine window
   uint32_t cbins_log2;   // candidate histogram bins used: the bracket's span >> sbin < 2^cbins_log2
-  uint32_t pad_;
+  uint32_t segs;         // sample segments per workgroup group (<= kSampleSegs): 2 up to 32 M
+                         // elements (more, shorter sample workgroups: a shorter bracket chain),
+                         // 4 above (fewer flushes; profiles/r05_ab_sample_segs.jsonl)
 };
 #ifndef FC_SAMPLE_SEGS_PER_WG
 #define FC_SAMPLE_SEGS_PER_WG 4
 #endif
-constexpr int kPilotSegs = FC_SAMPLE_SEGS_PER_WG;   // = kSampleSegs: the pilot IS workgroup 0's share
+constexpr int kPilotSegs = FC_SAMPLE_SEGS_PER_WG;   // >= P.segs: the pilot IS workgroup 0's share
 constexpr uint64_t kFullSampleMax = 1ull << 20;
 
 __host__ __device__ __forceinline__ uint64_t seg_start(const SamplePlan& P, uint32_t s) {

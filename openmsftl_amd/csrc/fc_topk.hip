@@ -339,7 +339,7 @@ __device__ __forceinline__ void sample_body(const T* __restrict__ g, const Sampl
       const uint32_t s = v + (uint32_t)q * P.pstride;
       es[q] = ls[q] = 0;
       xs[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (s < P.nseg) {
+      if ((uint32_t)q < P.segs && s < P.nseg) {
         seg_lane(P, s, tid, es[q], ls[q]);
         if (es[q] < ls[q]) xs[q] = load4_sample(g, es[q], ls[q]);
       }
@@ -407,7 +407,7 @@ __device__ __forceinline__ void sample_body(const T* __restrict__ g, const Sampl
         const uint32_t s = vn + (uint32_t)q * P.pstride;
         en[q] = ln[q] = 0;
         xn[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (vn < P.pstride && s < P.nseg) {
+        if ((uint32_t)q < P.segs && vn < P.pstride && s < P.nseg) {
           seg_lane(P, s, tid, en[q], ln[q]);
           if (en[q] < ln[q]) xn[q] = load4_sample(g, en[q], ln[q]);
         }
