@@ -777,13 +777,18 @@ int fc_qsgd_decode_accumulate(const fc_packet_view* views_dev, int m, uint64_t n
   FC_CHECK(m >= 1, "m=%d < 1", m);
   FC_CHECK(n >= 1 && n <= 0xffffffffull, "bad n");
   FC_CHECK(((uintptr_t)out & 15) == 0, "out must be 16-byte aligned");
-  QsgdDecodeArgs a;
-  memset(&a, 0, sizeof a);
-  a.views = views_dev; a.m = m; a.acc_in = continue_sum != 0; a.n = n; a.out = out;
   hipStream_t s = (hipStream_t)stream;
   TimedLaunch t(FC_TIME_DECODE, s);
-  hipLaunchKernelGGL(k_qsgd_decode<true>, dim3(stream_grid((n + 3) / 4)), dim3(kBlock), 0, s, a);
-  FC_LAUNCHED("k_qsgd_decode(acc)");
+  // kQsgdFoldM packets per launch (their parameters live in LDS); a longer fold continues the
+  // previous launch's partial sum in row order (the same additions as one launch)
+  for (int m0 = 0; m0 < m; m0 += kQsgdFoldM) {
+    QsgdDecodeArgs a;
+    memset(&a, 0, sizeof a);
+    a.views = views_dev + m0; a.m = std::min(kQsgdFoldM, m - m0);
+    a.acc_in = (m0 > 0 || continue_sum != 0) ? 1 : 0; a.n = n; a.out = out;
+    hipLaunchKernelGGL(k_qsgd_decode<true>, dim3(stream_grid((n + 3) / 4)), dim3(kBlock), 0, s, a);
+    FC_LAUNCHED("k_qsgd_decode(acc)");
+  }
   return FC_OK;
 }
 

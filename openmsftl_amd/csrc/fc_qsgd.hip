@@ -145,44 +145,76 @@ __device__ __forceinline__ float qsgd_value(uint32_t code, const QsgdParams& q) 
 }
 
 // ---- pass 2: quantise; thread = 8 consecutive elements -> 8 codes ----------------------------
+constexpr int kQsgdQuantUnroll = 2;            // groups per thread and pass, loads issued first
+__device__ __forceinline__ void qsgd_load8(const float* __restrict__ g, uint64_t e, uint64_t n,
+                                           float (&x)[8]) {
+  if (e + 8 <= n) {
+    const float4 a = load4_full(g + e), b = load4_full(g + e + 4);
+    x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = e + j < n ? g[e + j] : 0.f;
+  }
+}
+// The pass for one arithmetic form (F32: c32 finite, uniform per launch) and code width: one
+// branch per launch instead of both forms and the width tests per element.  (Measured and kept
+// out: one quad per thread, the quads of a wave contiguous, each quad computing its group's
+// Philox block: 127 -> 140 us at 128 M; without Philox or without the code arithmetic the pass
+// is 2-3 us shorter: it waits on memory, profiles/r05_ab_qsgd.jsonl.)
+template <bool F32, int W>
+__device__ __forceinline__ void qsgd_quant_pass(const float* __restrict__ g, uint64_t n,
+                                                uint64_t seed, uint64_t offset,
+                                                const QsgdParams& q, uint32_t* codes) {
+  const uint64_t groups = (n + kQsgdElems - 1) / kQsgdElems;
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  for (uint64_t t0 = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t0 < groups;
+       t0 += kQsgdQuantUnroll * stride) {
+    float xs[kQsgdQuantUnroll][8];
+#pragma unroll
+    for (int u = 0; u < kQsgdQuantUnroll; ++u)
+      if (t0 + u * stride < groups) qsgd_load8(g, (t0 + u * stride) * kQsgdElems, n, xs[u]);
+#pragma unroll
+    for (int u = 0; u < kQsgdQuantUnroll; ++u) {
+      const uint64_t t = t0 + u * stride;
+      if (t >= groups) break;
+      const uint64_t e = t * kQsgdElems;
+      const uint4 r0 = philox_block(e >> 3, seed, offset);     // 8 x 16 dither bits
+      const uint32_t wd[4] = {r0.x, r0.y, r0.z, r0.w};
+      uint32_t c[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t h = (wd[j >> 1] >> (16 * (j & 1))) & 0xffffu;
+        c[j] = e + j >= n ? 0u : qsgd_code<F32>(xs[u][j], h, q);
+      }
+      if (W == 4) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v |= c[j] << (4 * j);
+        codes[t] = v;
+      } else if (W == 8) {
+        reinterpret_cast<uint2*>(codes)[t] = make_uint2(c[0] | c[1] << 8 | c[2] << 16 | c[3] << 24,
+                                                        c[4] | c[5] << 8 | c[6] << 16 | c[7] << 24);
+      } else {
+        reinterpret_cast<uint4*>(codes)[t] = make_uint4(c[0] | c[1] << 16, c[2] | c[3] << 16,
+                                                        c[4] | c[5] << 16, c[6] | c[7] << 16);
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void k_qsgd_quant(const float* __restrict__ g, uint64_t n,
                                                        int bits, uint64_t seed, uint64_t offset,
                                                        const fc_packet_hdr* hdr, uint32_t* codes) {
   const QsgdParams q = qsgd_params(hdr->p, bits, n);
-  const uint64_t groups = (n + kQsgdElems - 1) / kQsgdElems;
-  for (uint64_t t0 = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t0 < groups;
-       t0 += (uint64_t)gridDim.x * kBlock) {
-    const uint64_t t = t0;
-    const uint64_t e = t * kQsgdElems;
-    float x[8];
-    if (e + 8 <= n) {
-      const float4 a = load4_full(g + e), b = load4_full(g + e + 4);
-      x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) x[j] = e + j < n ? g[e + j] : 0.f;
-    }
-    const uint4 r0 = philox_block(e >> 3, seed, offset);       // 8 x 16 dither bits
-    const uint32_t wd[4] = {r0.x, r0.y, r0.z, r0.w};
-    uint32_t c[8];
-    const bool f32 = q.c32 != __builtin_inff();
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const uint32_t h = (wd[j >> 1] >> (16 * (j & 1))) & 0xffffu;
-      c[j] = e + j >= n ? 0u : f32 ? qsgd_code<true>(x[j], h, q) : qsgd_code<false>(x[j], h, q);
-    }
-    if (q.width == 4) {
-      uint32_t v = 0;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v |= c[j] << (4 * j);
-      codes[t] = v;
-    } else if (q.width == 8) {
-      reinterpret_cast<uint2*>(codes)[t] = make_uint2(c[0] | c[1] << 8 | c[2] << 16 | c[3] << 24,
-                                                      c[4] | c[5] << 8 | c[6] << 16 | c[7] << 24);
-    } else {
-      reinterpret_cast<uint4*>(codes)[t] = make_uint4(c[0] | c[1] << 16, c[2] | c[3] << 16,
-                                                      c[4] | c[5] << 16, c[6] | c[7] << 16);
-    }
+  const bool f32 = q.c32 != __builtin_inff();
+  if (f32) {
+    if (q.width == 4) qsgd_quant_pass<true, 4>(g, n, seed, offset, q, codes);
+    else if (q.width == 8) qsgd_quant_pass<true, 8>(g, n, seed, offset, q, codes);
+    else qsgd_quant_pass<true, 16>(g, n, seed, offset, q, codes);
+  } else {
+    if (q.width == 4) qsgd_quant_pass<false, 4>(g, n, seed, offset, q, codes);
+    else if (q.width == 8) qsgd_quant_pass<false, 8>(g, n, seed, offset, q, codes);
+    else qsgd_quant_pass<false, 16>(g, n, seed, offset, q, codes);
   }
 }
 
@@ -219,43 +251,87 @@ __device__ __forceinline__ void qsgd_unpack4(const uint32_t* codes, uint64_t qd,
 // Thread = one quad of 4 elements: its codes are one 2 / 4 / 8-B load and its 4 values one
 // 16-B store, so every store instruction writes a contiguous 1 KB per wave.  (8 elements per
 // thread wrote two 16-B halves 32 B apart per lane: 146 us per 128 M decode with plain stores,
-// 239 us with non-temporal ones, which do not merge the halves.)
+// 239 us with non-temporal ones, which do not merge the halves.)  Each packet's scale and
+// width are computed once per workgroup (the fold: into LDS, kQsgdFoldM packets per launch;
+// the host splits a longer fold into continued launches), not per quad: re-reading the header
+// and an fp64 divide + sqrt per quad made the lone decode VALU-latency-bound (121 us at 128 M).
+// kQsgdDecUnroll quads per thread and pass, their code loads issued first.
+constexpr int kQsgdFoldM = 512;
+constexpr int kQsgdDecUnroll = 2;
+struct QsgdPkt {
+  const uint32_t* codes;
+  double scale;
+  float weight;
+  int width;
+};
+__device__ __forceinline__ float qsgd_value2(uint32_t code, double scale, int width) {
+  const uint32_t l = code & ((1u << (width - 1)) - 1u);
+  const double v = scale * (double)l;
+  return (float)(((code >> (width - 1)) & 1u) ? -v : v);
+}
 template <bool ACC>
 __global__ __launch_bounds__(kBlock) void k_qsgd_decode(QsgdDecodeArgs a) {
   const uint64_t n = a.n, quads = (n + 3) / 4;
   const int M = ACC ? a.m : 1;
-  for (uint64_t qd = (uint64_t)blockIdx.x * kBlock + threadIdx.x; qd < quads;
-       qd += (uint64_t)gridDim.x * kBlock) {
-    const uint64_t e = qd * 4;
-    const bool full = e + 4 <= n;
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    if (ACC && a.acc_in) {
-      if (full) {
-        const fc_f4v v = *(fc_gf4v*)(a.out + e);
-        acc[0] = v.x; acc[1] = v.y; acc[2] = v.z; acc[3] = v.w;
-      } else {
+  __shared__ QsgdPkt s_pk[ACC ? kQsgdFoldM : 1];
+  QsgdPkt one;
+  if (ACC) {
+    for (int m = threadIdx.x; m < M; m += kBlock) {
+      const fc_packet_view& v = a.views[m];
+      const QsgdParams q = qsgd_params(v.hdr->p, (int)v.hdr->k, n);
+      s_pk[m] = QsgdPkt{static_cast<const uint32_t*>(v.idx), q.scale, v.weight, q.width};
+    }
+    __syncthreads();
+  } else {
+    const QsgdParams q = qsgd_params(a.one.hdr->p, (int)a.one.hdr->k, n);
+    one = QsgdPkt{static_cast<const uint32_t*>(a.one.idx), q.scale, 1.0f, q.width};
+  }
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  for (uint64_t q0 = (uint64_t)blockIdx.x * kBlock + threadIdx.x; q0 < quads;
+       q0 += kQsgdDecUnroll * stride) {
+    float acc[kQsgdDecUnroll][4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) if (e + j < n) acc[j] = a.out[e + j];
+    for (int u = 0; u < kQsgdDecUnroll; ++u) {
+      const uint64_t qd = q0 + u * stride, e = qd * 4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[u][j] = 0.f;
+      if (ACC && a.acc_in && qd < quads) {
+        if (e + 4 <= n) {
+          const fc_f4v v = *(fc_gf4v*)(a.out + e);
+          acc[u][0] = v.x; acc[u][1] = v.y; acc[u][2] = v.z; acc[u][3] = v.w;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) if (e + j < n) acc[u][j] = a.out[e + j];
+        }
       }
     }
     for (int m = 0; m < M; ++m) {                                // rows in order (gar.py:44)
-      const fc_packet_view& v = ACC ? a.views[m] : a.one;
-      const fc_packet_hdr* h = v.hdr;
-      const QsgdParams q = qsgd_params(h->p, (int)h->k, n);
-      uint32_t c[4];
-      qsgd_unpack4(static_cast<const uint32_t*>(v.idx), qd, q.width, c);
+      const QsgdPkt& p = ACC ? s_pk[m] : one;
+      uint32_t c[kQsgdDecUnroll][4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float d = qsgd_value(c[j], q);
-        acc[j] = ACC ? __fadd_rn(acc[j], __fmul_rn(d, v.weight)) : d;
+      for (int u = 0; u < kQsgdDecUnroll; ++u)
+        if (q0 + u * stride < quads) qsgd_unpack4(p.codes, q0 + u * stride, p.width, c[u]);
+#pragma unroll
+      for (int u = 0; u < kQsgdDecUnroll; ++u) {
+        if (q0 + u * stride >= quads) break;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float d = qsgd_value2(c[u][j], p.scale, p.width);
+          acc[u][j] = ACC ? __fadd_rn(acc[u][j], __fmul_rn(d, p.weight)) : d;
+        }
       }
     }
-    if (full) {
-      __builtin_nontemporal_store(fc_f4v{acc[0], acc[1], acc[2], acc[3]},
-                                  reinterpret_cast<fc_f4v*>(a.out + e));
-    } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) if (e + j < n) a.out[e + j] = acc[j];
+    for (int u = 0; u < kQsgdDecUnroll; ++u) {
+      const uint64_t qd = q0 + u * stride, e = qd * 4;
+      if (qd >= quads) break;
+      if (e + 4 <= n) {
+        __builtin_nontemporal_store(fc_f4v{acc[u][0], acc[u][1], acc[u][2], acc[u][3]},
+                                    reinterpret_cast<fc_f4v*>(a.out + e));
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) if (e + j < n) a.out[e + j] = acc[u][j];
+      }
     }
   }
 }

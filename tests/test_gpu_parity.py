@@ -1003,6 +1003,23 @@ def test_qsgd_fedavg_and_statistics():
     assert (err < bound).mean() > 0.999
 
 
+def test_qsgd_fedavg_past_one_launch():
+    """fc_qsgd_decode_accumulate folds at most kQsgdFoldM = 512 packets per launch (their scales
+    in LDS) and continues the partial sum over longer folds: 700 packets (two launches) equal
+    the +0-started row-order sum of the oracle-decoded rows, bit for bit."""
+    from oracle import qsgd_oracle as qo
+    codec = _codec()
+    M, n, bits = 700, 4_099, 3
+    rng = np.random.default_rng(12)
+    grads = [(rng.standard_normal(n) * 10.0 ** rng.uniform(-3, 0)).astype(np.float32) for _ in range(M)]
+    pkts = [codec.encode_qsgd(torch.from_numpy(x).cuda(), bits, seed=i, offset=2)
+            for i, x in enumerate(grads)]
+    w = rng.uniform(0.01, 1, M).astype(np.float32)
+    agg = codec.decode_accumulate_qsgd(pkts, list(w)).cpu().numpy()
+    rows = [qo.decode(p.codes.cpu().numpy().view(np.uint32), n, bits, p.header().p) for p in pkts]
+    assert agg.tobytes() == go.sequential_weighted_sum(rows, w).tobytes()
+
+
 @pytest.mark.parametrize("n", [1, 1000])
 def test_qsgd_one_hot_keeps_its_element(n):
     """a one-hot gradient at bits = 14 lost its element (level s + 1 -> 0) about
