@@ -28,7 +28,7 @@ namespace fc {
 
 constexpr int kQsgdNormGrid = 1024;            // fixed: the fp64 sum order depends on it
 constexpr int kQsgdElems = 8;                  // elements per thread per step (quant/decode)
-constexpr int kQsgdNormUnroll = 4;             // float4 loads in flight per thread (norm pass)
+constexpr int kQsgdNormUnroll = 2;             // float4 loads in flight per thread (norm pass)
 // (Plain cache-allocating loads, so that a back-to-front quantise pass could re-read the norm
 // pass's tail from the Infinity Cache, measured slower: norm 98 -> 145 us at 128 M, and the
 // quantise no faster; profiles/r04_ab_qsgd.jsonl.)
@@ -57,8 +57,9 @@ __global__ __launch_bounds__(kBlock) void k_qsgd_norm(const float* __restrict__ 
   const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
   double acc = 0.0;
   const uint64_t n4 = n / 4, stride = (uint64_t)gridDim.x * kBlock;
-  // kQsgdNormUnroll float4 loads in flight per thread (one load per dependent fp64 chain step
-  // kept this pass latency-bound); the additions stay in the same per-thread order
+  // kQsgdNormUnroll float4 loads in flight per thread, the additions in a fixed per-thread
+  // order: 2 loads 89 us per 128 M pass, 1 or 4 loads 96-97 us, 2 loads on grids of 512 / 2048
+  // workgroups 94 / 102 us (profiles/r05_ab_qsgd.jsonl)
   uint64_t q = (uint64_t)blockIdx.x * kBlock + tid;
   for (; q + (kQsgdNormUnroll - 1) * stride < n4; q += kQsgdNormUnroll * stride) {
     float4 v[kQsgdNormUnroll];
@@ -145,7 +146,7 @@ __device__ __forceinline__ float qsgd_value(uint32_t code, const QsgdParams& q) 
 }
 
 // ---- pass 2: quantise; thread = 8 consecutive elements -> 8 codes ----------------------------
-constexpr int kQsgdQuantUnroll = 2;            // groups per thread and pass, loads issued first
+constexpr int kQsgdQuantUnroll = 1;            // groups per thread and pass, loads issued first
 __device__ __forceinline__ void qsgd_load8(const float* __restrict__ g, uint64_t e, uint64_t n,
                                            float (&x)[8]) {
   if (e + 8 <= n) {
@@ -157,46 +158,77 @@ __device__ __forceinline__ void qsgd_load8(const float* __restrict__ g, uint64_t
   }
 }
 // The pass for one arithmetic form (F32: c32 finite, uniform per launch) and code width: one
-// branch per launch instead of both forms and the width tests per element.  (Measured and kept
-// out: one quad per thread, the quads of a wave contiguous, each quad computing its group's
-// Philox block: 127 -> 140 us at 128 M; without Philox or without the code arithmetic the pass
-// is 2-3 us shorter: it waits on memory, profiles/r05_ab_qsgd.jsonl.)
+// branch per launch instead of both forms and the width tests per element.  Each load
+// instruction reads 1 KB contiguous per wave: 8 consecutive elements per lane as two 16-B
+// halves 32 B apart read 128 us per 128 M pass, the wave-contiguous halves and one DPP swap
+// 116 us.  (Measured and kept out: one quad per thread, each quad computing its group's Philox
+// block: 140 us; 4 groups per thread and pass: 129 us; without Philox or without the code
+// arithmetic the pass is 2-3 us shorter: it waits on memory, profiles/r05_ab_qsgd.jsonl.)
+__device__ __forceinline__ float4 qsgd_load4(const float* __restrict__ g, uint64_t e, uint64_t n) {
+  if (e + 4 <= n) return load4_full(g + e);
+  float4 v;
+  v.x = e < n ? g[e] : 0.f; v.y = e + 1 < n ? g[e + 1] : 0.f;
+  v.z = e + 2 < n ? g[e + 2] : 0.f; v.w = e + 3 < n ? g[e + 3] : 0.f;
+  return v;
+}
+__device__ __forceinline__ float qsgd_swap1(float v) {     // the value of lane ^ 1
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1,
+                                                            0xf, 0xf, true));
+}
 template <bool F32, int W>
 __device__ __forceinline__ void qsgd_quant_pass(const float* __restrict__ g, uint64_t n,
                                                 uint64_t seed, uint64_t offset,
                                                 const QsgdParams& q, uint32_t* codes) {
   const uint64_t groups = (n + kQsgdElems - 1) / kQsgdElems;
   const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-  for (uint64_t t0 = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t0 < groups;
-       t0 += kQsgdQuantUnroll * stride) {
-    float xs[kQsgdQuantUnroll][8];
-#pragma unroll
-    for (int u = 0; u < kQsgdQuantUnroll; ++u)
-      if (t0 + u * stride < groups) qsgd_load8(g, (t0 + u * stride) * kQsgdElems, n, xs[u]);
+  const uint32_t lane = threadIdx.x & 63u;
+  // A wave covers 64 consecutive groups (512 elements) per pass and loads them as two 1 KB
+  // contiguous 16-B-per-lane loads (lane l: elements 4l.. and 256 + 4l..); the lane pairs then
+  // swap halves so that lane 2m holds group m and lane 2m + 1 group 32 + m.
+  for (uint64_t w0 = (uint64_t)blockIdx.x * kBlock + (threadIdx.x & ~63u); w0 < groups;
+       w0 += kQsgdQuantUnroll * stride) {
+    float4 lo[kQsgdQuantUnroll], hi[kQsgdQuantUnroll];
 #pragma unroll
     for (int u = 0; u < kQsgdQuantUnroll; ++u) {
-      const uint64_t t = t0 + u * stride;
-      if (t >= groups) break;
+      const uint64_t e0 = (w0 + u * stride) * kQsgdElems;
+      if (e0 < n) {
+        lo[u] = qsgd_load4(g, e0 + 4 * lane, n);
+        hi[u] = qsgd_load4(g, e0 + 256 + 4 * lane, n);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kQsgdQuantUnroll; ++u) {
+      const uint64_t b = w0 + u * stride;
+      if (b >= groups) break;                                      // wave-uniform
+      const bool odd = lane & 1u;
+      const float4 give = odd ? lo[u] : hi[u];
+      float4 got;
+      got.x = qsgd_swap1(give.x); got.y = qsgd_swap1(give.y);
+      got.z = qsgd_swap1(give.z); got.w = qsgd_swap1(give.w);
+      const float4 a = odd ? got : lo[u], c = odd ? hi[u] : got;
+      const float xs[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+      const uint64_t t = b + (lane >> 1) + (odd ? 32u : 0u);
+      if (t >= groups) continue;
       const uint64_t e = t * kQsgdElems;
       const uint4 r0 = philox_block(e >> 3, seed, offset);     // 8 x 16 dither bits
       const uint32_t wd[4] = {r0.x, r0.y, r0.z, r0.w};
-      uint32_t c[8];
+      uint32_t c8[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const uint32_t h = (wd[j >> 1] >> (16 * (j & 1))) & 0xffffu;
-        c[j] = e + j >= n ? 0u : qsgd_code<F32>(xs[u][j], h, q);
+        c8[j] = e + j >= n ? 0u : qsgd_code<F32>(xs[j], h, q);
       }
       if (W == 4) {
         uint32_t v = 0;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v |= c[j] << (4 * j);
+        for (int j = 0; j < 8; ++j) v |= c8[j] << (4 * j);
         codes[t] = v;
       } else if (W == 8) {
-        reinterpret_cast<uint2*>(codes)[t] = make_uint2(c[0] | c[1] << 8 | c[2] << 16 | c[3] << 24,
-                                                        c[4] | c[5] << 8 | c[6] << 16 | c[7] << 24);
+        reinterpret_cast<uint2*>(codes)[t] = make_uint2(c8[0] | c8[1] << 8 | c8[2] << 16 | c8[3] << 24,
+                                                        c8[4] | c8[5] << 8 | c8[6] << 16 | c8[7] << 24);
       } else {
-        reinterpret_cast<uint4*>(codes)[t] = make_uint4(c[0] | c[1] << 16, c[2] | c[3] << 16,
-                                                        c[4] | c[5] << 16, c[6] | c[7] << 16);
+        reinterpret_cast<uint4*>(codes)[t] = make_uint4(c8[0] | c8[1] << 16, c8[2] | c8[3] << 16,
+                                                        c8[4] | c8[5] << 16, c8[6] | c8[7] << 16);
       }
     }
   }
@@ -269,19 +301,189 @@ __device__ __forceinline__ float qsgd_value2(uint32_t code, double scale, int wi
   const double v = scale * (double)l;
   return (float)(((code >> (width - 1)) & 1u) ? -v : v);
 }
+// The fold when every packet of the launch has code width W: lane = E = 128 / W consecutive
+// elements, so each packet's codes are ONE 16-B load per lane and 1 KB contiguous per wave
+// (the quad layout below reads 2 / 4 / 8 B per lane and packet: 675 us for 70 x 25.6 M 2-bit
+// packets, 1.3 TB/s of codes).  D packets' loads are issued before their additions, which
+// stay in row order per element (gar.py:44).  The E sums go out as E / 4 16-B stores per lane.
+template <int W>
+__device__ __forceinline__ void qsgd_fold_wide(const QsgdDecodeArgs& a, const QsgdPkt* pk, int M) {
+  constexpr int E = 128 / W, D = W == 4 ? 4 : W == 8 ? 4 : 2;
+  constexpr uint32_t mask = (1u << W) - 1u;
+  const uint64_t n = a.n;
+  const uint64_t words = (n + kQsgdElems - 1) / kQsgdElems * (uint64_t)(W / 4);   // code words
+  const uint64_t tiles = (n + E - 1) / E;                                          // lane tiles
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  for (uint64_t u = (uint64_t)blockIdx.x * kBlock + threadIdx.x; u < tiles; u += stride) {
+    const uint64_t e0 = u * E;
+    const bool full = e0 + E <= n;
+    float acc[E];
+#pragma unroll
+    for (int j = 0; j < E; ++j) acc[j] = 0.f;
+    if (a.acc_in) {
+      if (full) {
+#pragma unroll
+        for (int j = 0; j < E; j += 4) {
+          const fc_f4v v = *(const fc_gf4v*)(a.out + e0 + j);
+          acc[j] = v.x; acc[j + 1] = v.y; acc[j + 2] = v.z; acc[j + 3] = v.w;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < E; ++j) if (e0 + j < n) acc[j] = a.out[e0 + j];
+      }
+    }
+    const bool wfull = 4 * (u + 1) <= words;
+    for (int m0 = 0; m0 < M; m0 += D) {
+      fc_u32x4 c[D];
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        if (m0 + d >= M) break;
+        const uint32_t* cw = pk[m0 + d].codes;
+        if (wfull) {
+          c[d] = __builtin_nontemporal_load((const FC_G fc_u32x4*)cw + u);
+        } else {
+          uint32_t t[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) t[i] = 4 * u + i < words ? ((const FC_G uint32_t*)cw)[4 * u + i] : 0u;
+          c[d] = fc_u32x4{t[0], t[1], t[2], t[3]};
+        }
+      }
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        if (m0 + d >= M) break;
+        const QsgdPkt& p = pk[m0 + d];
+        const uint32_t cw4[4] = {c[d].x, c[d].y, c[d].z, c[d].w};
+#pragma unroll
+        for (int j = 0; j < E; ++j) {
+          const uint32_t code = (cw4[(j * W) >> 5] >> ((j * W) & 31)) & mask;
+          const float v = qsgd_value2(code, p.scale, W);
+          acc[j] = __fadd_rn(acc[j], __fmul_rn(v, p.weight));
+        }
+      }
+    }
+    if (full) {
+#pragma unroll
+      for (int j = 0; j < E; j += 4)
+        *(FC_G fc_f4v*)(a.out + e0 + j) = fc_f4v{acc[j], acc[j + 1], acc[j + 2], acc[j + 3]};
+    } else {
+#pragma unroll
+      for (int j = 0; j < E; ++j) if (e0 + j < n) a.out[e0 + j] = acc[j];
+    }
+  }
+}
+
+// Code widths 4 and 8 fold through per-packet tables: T_m[c] = fl(value(c) * w_m) for the
+// 2^W codes c, built in LDS by the workgroup (the same two roundings the per-element form does,
+// so the sums are bit-identical), then each element of each packet is one bit-field extract,
+// one LDS read and one addition.  (With the fp64 value per element the fold was VALU-bound:
+// 465 us for 70 x 25.6 M 2-bit packets, 270-285 us with the tables; 5-bit: 480 -> 415 us.)
+// kQsgdTabFloats floats of tables: 256 packets at W = 4, 16 at W = 8 per batch; a longer fold
+// rebuilds them per batch and tile.  D packets' code loads are issued together (loading the
+// next D while adding, or D = 2 / 8: no faster, profiles/r05_ab_qsgd.jsonl).
+constexpr int kQsgdTabFloats = 4096;
+template <int W>
+__device__ __forceinline__ void qsgd_fold_lut(const QsgdDecodeArgs& a, const QsgdPkt* pk, int M,
+                                              float* s_tab) {
+  constexpr int E = 128 / W, NT = 1 << W, B = kQsgdTabFloats / NT, D = 4;
+  constexpr uint32_t mask = NT - 1u;
+  const uint64_t n = a.n;
+  const uint64_t words = (n + kQsgdElems - 1) / kQsgdElems * (uint64_t)(W / 4);
+  const uint64_t tiles = (n + E - 1) / E;
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  const uint64_t first = (uint64_t)blockIdx.x * kBlock;
+  for (uint64_t ub = first; ub < tiles; ub += stride) {         // workgroup-uniform
+    const uint64_t u = ub + threadIdx.x, e0 = u * E;
+    const bool active = u < tiles, full = e0 + E <= n, wfull = 4 * (u + 1) <= words;
+    float acc[E];
+#pragma unroll
+    for (int j = 0; j < E; ++j) acc[j] = 0.f;
+    if (active && a.acc_in) {
+      if (full) {
+#pragma unroll
+        for (int j = 0; j < E; j += 4) {
+          const fc_f4v v = *(const fc_gf4v*)(a.out + e0 + j);
+          acc[j] = v.x; acc[j + 1] = v.y; acc[j + 2] = v.z; acc[j + 3] = v.w;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < E; ++j) if (e0 + j < n) acc[j] = a.out[e0 + j];
+      }
+    }
+    for (int mb = 0; mb < M; mb += B) {
+      const int nb = M - mb < B ? M - mb : B;
+      if (ub == first || M > B) {                               // (re)build this batch's tables
+        __syncthreads();
+        for (int i = threadIdx.x; i < nb * NT; i += kBlock) {
+          const QsgdPkt& p = pk[mb + i / NT];
+          s_tab[i] = __fmul_rn(qsgd_value2((uint32_t)(i % NT), p.scale, W), p.weight);
+        }
+        __syncthreads();
+      }
+      if (!active) continue;
+      auto load_group = [&](int m0, fc_u32x4 (&c)[D]) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+          if (m0 + d >= nb) break;
+          const uint32_t* cw = pk[mb + m0 + d].codes;
+          if (wfull) {
+            c[d] = __builtin_nontemporal_load((const FC_G fc_u32x4*)cw + u);
+          } else {
+            uint32_t t[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) t[i] = 4 * u + i < words ? ((const FC_G uint32_t*)cw)[4 * u + i] : 0u;
+            c[d] = fc_u32x4{t[0], t[1], t[2], t[3]};
+          }
+        }
+      };
+      fc_u32x4 c[D];
+      load_group(0, c);
+      for (int m0 = 0; m0 < nb; m0 += D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+          if (m0 + d >= nb) break;
+          const float* tab = s_tab + (m0 + d) * NT;
+          const uint32_t cw4[4] = {c[d].x, c[d].y, c[d].z, c[d].w};
+#pragma unroll
+          for (int j = 0; j < E; ++j)
+            acc[j] = __fadd_rn(acc[j], tab[(cw4[(j * W) >> 5] >> ((j * W) & 31)) & mask]);
+        }
+        if (m0 + D < nb) load_group(m0 + D, c);
+      }
+    }
+    if (!active) continue;
+    if (full) {
+#pragma unroll
+      for (int j = 0; j < E; j += 4)
+        *(FC_G fc_f4v*)(a.out + e0 + j) = fc_f4v{acc[j], acc[j + 1], acc[j + 2], acc[j + 3]};
+    } else {
+#pragma unroll
+      for (int j = 0; j < E; ++j) if (e0 + j < n) a.out[e0 + j] = acc[j];
+    }
+  }
+}
+
 template <bool ACC>
 __global__ __launch_bounds__(kBlock) void k_qsgd_decode(QsgdDecodeArgs a) {
   const uint64_t n = a.n, quads = (n + 3) / 4;
   const int M = ACC ? a.m : 1;
   __shared__ QsgdPkt s_pk[ACC ? kQsgdFoldM : 1];
+  __shared__ float s_tab[ACC ? kQsgdTabFloats : 1];
   QsgdPkt one;
   if (ACC) {
+    const int w0 = qsgd_width((int)a.views[0].hdr->k);
+    int same = 1;
     for (int m = threadIdx.x; m < M; m += kBlock) {
       const fc_packet_view& v = a.views[m];
       const QsgdParams q = qsgd_params(v.hdr->p, (int)v.hdr->k, n);
       s_pk[m] = QsgdPkt{static_cast<const uint32_t*>(v.idx), q.scale, v.weight, q.width};
+      same &= q.width == w0;
     }
-    __syncthreads();
+    if (__syncthreads_and(same)) {                     // one width in the launch: wide loads
+      if (w0 == 4) qsgd_fold_lut<4>(a, s_pk, M, s_tab);
+      else if (w0 == 8) qsgd_fold_lut<8>(a, s_pk, M, s_tab);
+      else qsgd_fold_wide<16>(a, s_pk, M);
+      return;
+    }
   } else {
     const QsgdParams q = qsgd_params(a.one.hdr->p, (int)a.one.hdr->k, n);
     one = QsgdPkt{static_cast<const uint32_t*>(a.one.idx), q.scale, 1.0f, q.width};

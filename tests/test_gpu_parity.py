@@ -1020,6 +1020,32 @@ def test_qsgd_fedavg_past_one_launch():
     assert agg.tobytes() == go.sequential_weighted_sum(rows, w).tobytes()
 
 
+@pytest.mark.parametrize("bits_of", ["w4", "w8", "w16", "mixed"])
+@pytest.mark.parametrize("n", [37, 65_541])
+def test_qsgd_fedavg_each_code_width(bits_of, n):
+    """The fold reads a launch's codes 16 B per lane when all its packets share one code width
+    (4 / 8 / 16 bits: 32 / 16 / 8 elements per lane) and per quad otherwise: each equals the
+    +0-started row-order sum of the oracle-decoded rows, bit for bit, on ragged n (a partial
+    last lane and a partial last code word), and continue_sum folds into a partial sum."""
+    from oracle import qsgd_oracle as qo
+    codec = _codec()
+    M = 11
+    bits = {"w4": [2] * M, "w8": [5] * M, "w16": [12] * M,
+            "mixed": [[2, 5, 12, 3][i % 4] for i in range(M)]}[bits_of]
+    rng = np.random.default_rng(n + M)
+    grads = [(rng.standard_normal(n) * 10.0 ** rng.uniform(-3, 0)).astype(np.float32) for _ in range(M)]
+    pkts = [codec.encode_qsgd(torch.from_numpy(x).cuda(), b, seed=i, offset=4)
+            for i, (x, b) in enumerate(zip(grads, bits))]
+    w = rng.uniform(0.01, 1, M).astype(np.float32)
+    rows = [qo.decode(p.codes.cpu().numpy().view(np.uint32), n, b, p.header().p)
+            for p, b in zip(pkts, bits)]
+    agg = codec.decode_accumulate_qsgd(pkts, list(w)).cpu().numpy()
+    assert agg.tobytes() == go.sequential_weighted_sum(rows, w).tobytes()
+    part = codec.decode_accumulate_qsgd(pkts[:4], list(w[:4]))
+    codec.decode_accumulate_qsgd(pkts[4:], list(w[4:]), out=part, continue_sum=True)
+    assert part.cpu().numpy().tobytes() == agg.tobytes()
+
+
 @pytest.mark.parametrize("n", [1, 1000])
 def test_qsgd_one_hot_keeps_its_element(n):
     """a one-hot gradient at bits = 14 lost its element (level s + 1 -> 0) about

@@ -20,6 +20,9 @@ def main():
     ap.add_argument("--bits", type=int, default=2)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--tag", default="")
+    ap.add_argument("--fold", type=int, default=0, help="also time a FedAVG fold of this many "
+                    "packets of --fold-n elements (decode_accumulate_qsgd)")
+    ap.add_argument("--fold-n", type=int, default=25_557_032)
     a = ap.parse_args()
     import torch
     from openmsftl_amd import _lib as L
@@ -46,9 +49,26 @@ def main():
             step()
         torch.cuda.synchronize()
     res = {c: round(kt.avg_us(c), 2) for c in L.TIME_CLASSES if kt.launches.get(c)}
+    fold = None
+    if a.fold:
+        del g, out, pkt
+        torch.cuda.empty_cache()
+        gf = torch.randn(a.fold_n, device="cuda", generator=torch.Generator(device="cuda").manual_seed(3))
+        pk = [codec.encode_qsgd(gf, a.bits, seed=i) for i in range(a.fold)]
+        w = [1.0 / a.fold] * a.fold
+        acc = codec.decode_accumulate_qsgd(pk, w)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(5):
+            codec.decode_accumulate_qsgd(pk, w, out=acc)
+        torch.cuda.synchronize()
+        fus = (time.perf_counter() - t0) / 5 * 1e6
+        code_b = pk[0].codes.numel() * pk[0].codes.element_size()
+        fold = {"m": a.fold, "n": a.fold_n, "us": round(fus, 1),
+                "GBps_codes": round(a.fold * code_b / fus / 1e3, 1)}
     alg = 13.0 * a.n if a.bits <= 2 else None      # bench.py qsgd_single's algorithmic bytes
     print(json.dumps({"tag": a.tag, "n": a.n, "bits": a.bits, "avg_us": res, "wall_us": round(wall, 1),
-                      "hbm_frac": round(alg / wall / 8e6, 4) if alg else None}), flush=True)
+                      "hbm_frac": round(alg / wall / 8e6, 4) if alg else None, "fold": fold}), flush=True)
 
 
 if __name__ == "__main__":
