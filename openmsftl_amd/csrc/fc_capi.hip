@@ -77,27 +77,17 @@ static uint32_t decode_grid(uint64_t n, uint32_t per_cu = kDecBlocksPerCU) {
   return g < nch ? g : nch;
 }
 
-#ifndef FC_MAX_SAMPLE_SEGS
-#define FC_MAX_SAMPLE_SEGS 1024
-#endif
-#ifndef FC_SAMPLE_DIV
-#define FC_SAMPLE_DIV 64                          // sample 1/64 of the gradient (below the cap)
-#endif
+constexpr int FC_MAX_SAMPLE_SEGS = 1024;
+constexpr int FC_SAMPLE_DIV = 64;                          // sample 1/64 of the gradient (below the cap)
 // fc_topk_encode_dense (the drop-in compress('top') path) samples more: its sample latency
 // hides under the fused launch's first round of chunk loads, and a narrower bracket means
 // fewer candidates on its critical path (16 M: 256 -> 512 segments took 68.8 -> 60.8 us; the
 // 128-client bench step got slower with a bigger sample: profiles/r02_ab_sample_plan.jsonl).
 // Its dense result does not depend on the bracket; packet encodes keep the batched plan, so a
 // single encode_top and a batched one write the same packet bytes (slack included).
-#ifndef FC_SAMPLE_DIV_SINGLE
-#define FC_SAMPLE_DIV_SINGLE 32
-#endif
-#ifndef FC_MAX_SAMPLE_SEGS_SINGLE
-#define FC_MAX_SAMPLE_SEGS_SINGLE 2048
-#endif
-#ifndef FC_SAMPLE_ROUNDS
-#define FC_SAMPLE_ROUNDS 4                        // sample groups per batched k_sample1 workgroup
-#endif
+constexpr int FC_SAMPLE_DIV_SINGLE = 32;
+constexpr int FC_MAX_SAMPLE_SEGS_SINGLE = 2048;
+constexpr int FC_SAMPLE_ROUNDS = 4;                        // sample groups per batched k_sample1 workgroup
 // Candidate-histogram bins a batched encode's bracket is cut into: ~kCandPerBin expected
 // candidates per bin, 256..4096 bins.  Every batched resolve workgroup flushes that many
 // coalesced bins and the survivors of one bin are sorted on the chain, so fewer, fuller bins
@@ -106,9 +96,7 @@ static uint32_t decode_grid(uint64_t n, uint32_t per_cu = kDecBlocksPerCU) {
 // resolve slower, 151 -> 158 us per 64 clients, profiles/r05_ab_cand_bins.jsonl).  A lone
 // encode keeps 4096: its compaction bins every candidate with a device atomic, and fewer bins
 // queue more of them on one address (128 M packet encode 167 -> 277 us with 1024).
-#ifndef FC_CAND_PER_BIN
-#define FC_CAND_PER_BIN 128
-#endif
+constexpr int FC_CAND_PER_BIN = 128;
 static uint32_t cand_bins_log2(uint64_t n, const SamplePlan& P) {
   if (P.full || P.lo_all || P.hi_none) return 12;
   const double S = (double)P.nseg * 1024.0;
@@ -340,9 +328,7 @@ static uint32_t resolve_grid(uint32_t nchunks, uint32_t want) {
   return g > need ? g : need;
 }
 
-#ifndef FC_RESOLVE_CPW
-#define FC_RESOLVE_CPW 8          // lone encode: >= this many chunks per k_resolve workgroup
-#endif
+constexpr int FC_RESOLVE_CPW = 8;          // lone encode: >= this many chunks per k_resolve workgroup
 // k_resolve<true> (a.rbin: the compaction left the binning to the resolve) then k_resolve<false>:
 // no workgroup of either launch waits for another (only last-arriver tickets), so they are
 // safe beside any other kernel, encodes on other streams included
@@ -723,15 +709,9 @@ size_t fc_qsgd_workspace_bytes(void) { return 64 + 8 * (size_t)kQsgdNormGrid; }
 
 // Grid caps of the QSGD passes (grid-stride loops): quantise 8192 workgroups (113 us per 128 M,
 // 4096: 116, 1024: 138), lone decode 1024 (99 us, 4096: 111), fold one lane tile per thread.
-#ifndef FC_QSGD_QGRID
-#define FC_QSGD_QGRID 8192
-#endif
-#ifndef FC_QSGD_DGRID
-#define FC_QSGD_DGRID 1024
-#endif
-#ifndef FC_QSGD_FGRID
-#define FC_QSGD_FGRID 65535
-#endif
+constexpr int FC_QSGD_QGRID = 8192;
+constexpr int FC_QSGD_DGRID = 1024;
+constexpr int FC_QSGD_FGRID = 65535;
 static uint32_t stream_grid(uint64_t items, uint64_t cap) {
   uint64_t b = (items + kBlock - 1) / kBlock;
   if (b < 1) b = 1;

@@ -22,13 +22,9 @@ constexpr int kHistBins = 1 << kHistBits;   // 4096
 constexpr int kSmallCap = 4096;             // exact-finish list (LDS bitonic, 32 KiB)
 constexpr int kEngineGrid = 256;            // radix-engine workgroups (one per CU)
 constexpr int kEnginePasses = 6;            // ceil(63 / 12): enough for any comp width
-#ifndef FC_RESOLVE_GRID
-#define FC_RESOLVE_GRID 256
-#endif
+constexpr int FC_RESOLVE_GRID = 256;
 constexpr int kResolveGrid = FC_RESOLVE_GRID;           // k_resolve workgroups
-#ifndef FC_RESOLVE_GRID_BATCH
-#define FC_RESOLVE_GRID_BATCH 16
-#endif
+constexpr int FC_RESOLVE_GRID_BATCH = 16;
 constexpr int kResolveGridBatch = FC_RESOLVE_GRID_BATCH;   // k_resolve workgroups per client (batched encode;
                                                           // 16 vs 64: configs[2] +2.1 %, configs[3] +0.2 %)
 constexpr int kSlots = kVec * kWaves;       // 32 (i, w) slots per chunk

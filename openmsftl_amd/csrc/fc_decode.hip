@@ -88,14 +88,10 @@ struct DecodeArgs {
 constexpr int kDBlock = 256;                   // decode workgroup (4 waves)
 constexpr int kDVec = kChunk / (kDBlock * 4);  // 8 float4 per thread: e = i*1024 + w*256 + lane*4
 constexpr int kDecR = 4;                       // slot entries per thread per item (1024 / chunk)
-#ifndef FC_DEC_GROUP
-#define FC_DEC_GROUP 4
-#endif
+constexpr int FC_DEC_GROUP = 4;
 constexpr int kDecGroup = FC_DEC_GROUP;        // items whose loads are issued together
 constexpr int kDecMaxM = 64;                   // packets per launch (the host splits larger batches)
-#ifndef FC_SPARSE_MAXM
-#define FC_SPARSE_MAXM 128
-#endif
+constexpr int FC_SPARSE_MAXM = 128;
 // k_decode_sparse: packets per launch.  Every launch after the first re-reads and re-writes the
 // 4N-byte aggregate, so a whole 128-client batch is folded in one launch (uint8 fold counts
 // in cntC stay exact up to 255).
@@ -391,9 +387,7 @@ __global__ __launch_bounds__(kDBlock, kDecBlocksPerCU) void k_decode(DecodeArgs 
 // --------------------------------------------------------------------------------------
 constexpr int kSBlock = 256;
 constexpr int kSR = 4;                         // entries per thread per item (1024 per item)
-#ifndef FC_SGROUP
-#define FC_SGROUP 4
-#endif
+constexpr int FC_SGROUP = 4;
 constexpr int kSGroup = FC_SGROUP;             // items whose loads are issued together
 constexpr int kSBlocksPerCU = 3;               // 47 KB LDS per workgroup (4 per CU with the
                                                // poison counts dropped measured no faster)
@@ -650,21 +644,15 @@ __global__ __launch_bounds__(kSBlock, kSBlocksPerCU) void k_decode_sparse(Decode
 // --------------------------------------------------------------------------------------
 constexpr int kQBlock = 256;
 constexpr int kQuarter = kChunk / 4;
-#ifndef FC_QR
-#define FC_QR 4
-#endif
+constexpr int FC_QR = 4;
 constexpr int kQR = FC_QR;                      // entry rounds (x64 lanes) loaded per item: 256
                                                 // entries (a quarter holds ~205 at f = 0.1; the
                                                 // rare longer item folds its rest in a tail
                                                 // loop: 4 rounds + tail 17.7 us/packet against
                                                 // 5 rounds 19.9, 5 + tail 18.6)
-#ifndef FC_QG
-#define FC_QG 3
-#endif
+constexpr int FC_QG = 3;
 constexpr int kQGroup = FC_QG;                  // items per load group
-#ifndef FC_QTAIL
-#define FC_QTAIL 8
-#endif
+constexpr int FC_QTAIL = 8;
 // FC_QTAIL > kQR: an item holding more than kQR * 64 entries folds the rest in a tail loop
 // right after its rounds; only a quarter above FC_QTAIL * 64 entries takes the slow body
 constexpr int kQTail = FC_QTAIL > FC_QR ? FC_QTAIL : FC_QR;

@@ -318,9 +318,7 @@ struct Fast64Args {
   uint32_t* status;            // caller's device word: FC_STATUS_OK / RETRY_EXACT
 };
 
-#ifndef FC_F64_DELAY
-#define FC_F64_DELAY 90               // k_fused64's first-round chunks: s_sleep before loading
-#endif
+constexpr int FC_F64_DELAY = 90;               // k_fused64's first-round chunks: s_sleep before loading
 
 // One workgroup per 8192-element chunk: 16 double2 per thread, coalesced (element
 // base + 2 (i * 256 + tid) + {0, 1}).
@@ -424,9 +422,7 @@ __global__ __launch_bounds__(kBlock) void k_fused64(Fast64Args a, SamplePlan P, 
   }
   const uint32_t chunk = blockIdx.x - nsamp;
   fc_d2v x[kI64];
-#if FC_F64_DELAY
   if (chunk < 1024u) __builtin_amdgcn_s_sleep(FC_F64_DELAY);   // the sample's loads first
-#endif
   load64_chunk(a, chunk, x);
   if (threadIdx.x == 0) {
     const uint32_t* rec = &W.pub[(blockIdx.x % kPubCopies) * kPubStride];

@@ -302,9 +302,7 @@ __device__ __forceinline__ void pred_body(const PredArgs& a, uint32_t chunk, Pre
 }
 
 // rand-k's occupancy (its Philox rounds, unrolled four at a time, once spilled 39 VGPRs)
-#ifndef FC_PRED_PHILOX_WAVES
-#define FC_PRED_PHILOX_WAVES 8
-#endif
+constexpr int FC_PRED_PHILOX_WAVES = 8;
 template <int SRC, int FMT>
 __global__ __launch_bounds__(kCBlock, SRC == kSrcPhiloxKey ? FC_PRED_PHILOX_WAVES : FC_MAG1_WAVES_PER_EU) void k_compact_pred(PredArgs a) {
   __shared__ __attribute__((aligned(16))) PredShared sh;

@@ -43,12 +43,8 @@ static_assert(sizeof(TopkState) <= 1024, "state block");
 // 52 us with ONE sample shard for its 128 sample workgroups, 128 M best at two; the batched
 // resolve 84 -> 78 us and the lone packet resolve 24 -> 23 us with two candidate shards (one:
 // 26 us); eight candidate shards +50 %.
-#ifndef FC_SAMPLE_SHARDS
-#define FC_SAMPLE_SHARDS 2
-#endif
-#ifndef FC_CAND_SHARDS
-#define FC_CAND_SHARDS 2
-#endif
+constexpr int FC_SAMPLE_SHARDS = 2;
+constexpr int FC_CAND_SHARDS = 2;
 constexpr int kSampleShards = FC_SAMPLE_SHARDS;   // k_sample1's global histogram, sharded by workgroup
 constexpr int kCandShards = FC_CAND_SHARDS;       // k_resolve's candidate histogram, likewise
 constexpr int kTickGroups = 16;             // two-level last-arriver tickets (fc_common.h)
@@ -146,9 +142,7 @@ struct SamplePlan {
                          // elements (more, shorter sample workgroups: a shorter bracket chain),
                          // 4 above (fewer flushes; profiles/r05_ab_sample_segs.jsonl)
 };
-#ifndef FC_SAMPLE_SEGS_PER_WG
-#define FC_SAMPLE_SEGS_PER_WG 4
-#endif
+constexpr int FC_SAMPLE_SEGS_PER_WG = 4;
 constexpr int kPilotSegs = FC_SAMPLE_SEGS_PER_WG;   // >= P.segs: the pilot IS workgroup 0's share
 constexpr uint64_t kFullSampleMax = 1ull << 20;
 

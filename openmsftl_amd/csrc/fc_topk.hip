@@ -1025,12 +1025,8 @@ __device__ __forceinline__ void compact_mag_item(const CompactArgs& a0, const Ma
   }
 }
 
-#ifndef FC_MAG1_WAVES_PER_EU
-#define FC_MAG1_WAVES_PER_EU 8
-#endif
-#ifndef FC_MAG1_IL
-#define FC_MAG1_IL 64
-#endif
+constexpr int FC_MAG1_WAVES_PER_EU = 8;
+constexpr int FC_MAG1_IL = 64;
 // Dispatch order: workgroups are dispatched x-fastest, so the chunks of FC_MAG1_IL clients are
 // interleaved (chunk-major within a group of clients): FC_MAG1_IL address streams are in
 // flight at once instead of one.  Measured (tools/kbench.py --batch 64, 128 M floats): IL 1 / 4

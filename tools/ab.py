@@ -8,7 +8,7 @@
 Every probe is a script that accepts ``--lib PATH`` and ``--tag TAG`` and prints one JSON line
 (tools/sample_probe.py, tools/kbench.py, bench.py with ``--lib``).  Variants run in turn, in
 alternating order on every repetition (boxes differ by 2-4 %: compare only within one call).
-Variants are built with tools/mkvar.sh (``-D`` flags into tools/variants/lib_<name>.so);
+Variants are built with tools/mkvar.sh (``FC_NAME=VALUE`` constants into tools/variants/lib_<name>.so);
 ``name=`` (empty path) is the default in-tree build.  Each result line gets ``var``, ``probe``
 and ``rep``; a failing probe stops the run (no retries on the GPU).
 """

@@ -1,9 +1,9 @@
-# Build a diagnostic / A-B variant of libfedcodec.so: tools/mkvar.sh <name> [-DFLAG=...]...
-# -> tools/variants/lib_<name>.so (git-ignored; travels to the GPU box with the tree).
+# Build a diagnostic / A-B variant of libfedcodec.so: tools/mkvar.sh <name> [FC_NAME=VALUE]...
+# [-DFLAG]...  FC_NAME=VALUE rewrites the tuned constant `constexpr int FC_NAME = ...;` in a
+# copy of the sources (the product source carries no -D switches); -D flags (FC_TRACE,
+# FC_DEBUG_BUILD) go to hipcc.  -> tools/variants/lib_<name>.so (git-ignored; travels to the
+# GPU box with the tree).
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 NAME=$1; shift
-mkdir -p "$ROOT/tools/variants"
-/opt/rocm/bin/hipcc -O3 -std=c++17 -ffp-contract=off -fPIC -shared --offload-arch=gfx950 \
-  -Wno-unused-function "$@" -o "$ROOT/tools/variants/lib_$NAME.so" "$ROOT/openmsftl_amd/csrc/fedcodec.hip"
-echo "built tools/variants/lib_$NAME.so ($*)"
+exec bash "$ROOT/tools/patchvar.sh" "$NAME" "$ROOT/tools/edits/none.py" "$@"
