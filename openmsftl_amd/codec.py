@@ -259,10 +259,14 @@ _MAX_SIDE = 4          # GPU_MAX_HW_QUEUES is 4: more forked streams would share
 # interleaved, so an XCD can fill up with waiters whose partners are queued on another full
 # XCD (round 4 measured this stall, to the spin bound, with the then-waiting k_resolve).  Every
 # fused encode on a device is therefore queued after the device's previous one when that one
-# went to another stream: an event recorded right after each fused encode (so a later encode
-# waits for that encode only, not for work queued behind it).  Every other encode kernel —
-# batched, mask, rand-k, fp64, exact — has only last-arriver tickets and runs beside anything.
-_FUSED_LAST: dict = {}                  # device index -> (stream, event after its last fused encode)
+# went to another stream: the device remembers the stream of its last fused encode, and a
+# fused encode on ANOTHER stream records an event on that stream at that moment and waits for
+# it (everything queued there so far, the previous fused encode included).  Calls on one stream
+# record nothing: an event recorded after every fused encode cost ~3 us per call at 16 M
+# (dense 47.9 -> 44.2-45.0 us, the HIP-graph figure; profiles/r05_ab_order_events.jsonl).
+# Every other encode kernel — batched, mask, rand-k, fp64, exact — has only last-arriver
+# tickets and runs beside anything.
+_FUSED_LAST: dict = {}                  # device index -> stream of its last fused encode
 _FUSED_LOCK = threading.RLock()
 
 
@@ -277,12 +281,12 @@ def _fused_encode(dev: torch.device):
         return
     with _FUSED_LOCK:
         last = _FUSED_LAST.get(key)
-        if last is not None and last[0] != stream:
-            stream.wait_event(last[1])
+        if last is not None and last != stream:
+            ev = torch.cuda.Event()
+            ev.record(last)
+            stream.wait_event(ev)
         yield
-        ev = last[1] if last is not None else torch.cuda.Event()
-        ev.record(stream)
-        _FUSED_LAST[key] = (stream, ev)
+        _FUSED_LAST[key] = stream
 
 
 def _side_streams(dev: torch.device, count: int = 2) -> list:

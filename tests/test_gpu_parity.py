@@ -547,6 +547,46 @@ def test_fused_encodes_on_concurrent_streams_are_bounded(monkeypatch):
     print(f"encodes that stalled to the poll bound (RETRY, re-encoded): {retries} of 400")
 
 
+def test_fused_encodes_ordered_across_streams():
+    """codec's own ordering of fused encodes: a fused encode on another stream than the
+    device's previous one records an event on that stream when it is issued and waits for it
+    (calls on one stream record nothing).  Alternating a packet encode and a dense one over two
+    streams 200 times, with other work queued behind each, never stalls (every status OK) and
+    both results equal the single-stream encodes'."""
+    codec = _codec()
+    n, f = 1 << 24, 0.1
+    gen = torch.Generator(device="cuda").manual_seed(18)
+    g0 = torch.randn(n, device="cuda", generator=gen) * 1e-3
+    g1 = torch.randn(n, device="cuda", generator=gen) * 3e-2
+    k = co.effective_k(co.num_kept(f, n), n)
+    ref0 = _packet_bytes(codec.encode_top(g0, k))
+    ref1 = codec.decode(codec.encode_top(g1, k)).clone()
+    s0, s1 = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s0):
+        p0 = codec.encode_top(g0, k, check=False)
+        bad0 = torch.zeros((), dtype=torch.int64, device="cuda")
+        junk0 = torch.empty_like(g0)
+    with torch.cuda.stream(s1):
+        p1 = codec.Packet.alloc(n, codec.L.FC_FMT_IDXVAL, g1.device, k=k)
+        out1 = torch.empty_like(g1)
+        bad1 = torch.zeros((), dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    for i in range(200):
+        with torch.cuda.stream(s0):
+            codec.encode_top(g0, k, packet=p0, check=False)
+            bad0 += (p0.hdr[36:40] != 0).any().to(torch.int64)
+            if i % 3 == 0:
+                codec.decode(p0, out=junk0)          # work queued behind the encode
+        with torch.cuda.stream(s1):
+            codec.compress_top_dense(g1, k, out=out1, packet=p1, check=False)
+            bad1 += (p1.hdr[36:40] != 0).any().to(torch.int64)
+    torch.cuda.synchronize()
+    assert int(bad0) == 0 and int(bad1) == 0
+    assert _packet_bytes(p0) == ref0
+    assert torch.equal(out1.view(torch.int32), ref1.view(torch.int32))
+
+
 @pytest.mark.parametrize("M,streams", [(5, 2), (7, 3), (2, 2), (1, 2)])
 def test_encode_fold_batch_pipelined(M, streams):
     """encode_fold_batch (each sub-batch folded on its stream as soon as it is encoded, the

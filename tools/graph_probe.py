@@ -16,9 +16,14 @@ def main():
     ap.add_argument("--calls", type=int, default=20)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--tag", default="")
+    ap.add_argument("--no-order-events", action="store_true",
+                    help="A/B only: replace codec._fused_encode's per-call event with nothing")
     args = ap.parse_args()
+    import contextlib
     import torch
     from openmsftl_amd import codec
+    if args.no_order_events:
+        codec._fused_encode = contextlib.contextmanager(lambda dev: (yield))
     from openmsftl_amd.compression import kept_count
     n, k = args.n, kept_count(0.1, args.n)
     g = torch.randn(n, device="cuda", generator=torch.Generator(device="cuda").manual_seed(1)) * 1e-2
