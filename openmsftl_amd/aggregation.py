@@ -327,7 +327,11 @@ def aggregate_grads(self, clients: List, input_feature: np.ndarray = None,
     w = getattr(self.gar, "gradient_weights", None)
     f32_weights = w is None or np.asarray(w).dtype == np.float32
     plan = None
-    if device_gar and grad0.dtype == np.float32 and f32_weights and n > 0:
+    # stream only when EVERY row is a float32 gradient: a float64 client after a float32 one
+    # (RandomGaussian Byzantine noise, attack_models.py:105-118) is compressed in its own dtype
+    # and cast into G's float32 row by the generic path, as aggregation.py:63 does
+    all_f32 = all(np.asarray(c.grad).dtype == np.float32 for c in clients)
+    if device_gar and all_f32 and f32_weights and n > 0:
         plan = row_plan(clients, n)
     if plan is not None:
         # streamed from the host gradients, G never built (rows live group by group)

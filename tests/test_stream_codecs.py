@@ -364,3 +364,27 @@ def test_aggregator_generic_path_folds_rows(kind):
     assert agg.agg_path == "dense-fold" and agg.curr_G is None
     assert agg.agg_grad.dtype == want.dtype
     assert agg.agg_grad.tobytes() == want.tobytes()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["full", "top", "dropout-unbiased"])
+def test_aggregator_mixed_dtype_round_takes_the_generic_path(name):
+    """client 0 float32, later clients float64 (RandomGaussian Byzantine
+    noise with noise_scale == 0, attack_models.py:105-118).  G = zeros(dtype=float32)
+    (aggregation.py:59) and each float64 row is compressed in its own dtype, then cast into G
+    (:63): the round must not stream, and agg_grad equals the oracle's FedAVG of that G."""
+    pytest.importorskip("torch")
+    from openmsftl_amd import Compression
+    from openmsftl_amd.aggregation import Aggregator
+    grads = _grads(6, N, seed=41)
+    for j in (2, 5):
+        grads[j] = grads[j].astype(np.float64) * (1.0 + 1e-9)   # genuinely float64 values
+    seed = 23
+    want, nxt = _reference_round([CFGS[name]] * 6, grads, seed)
+    agg = Aggregator({"aggregation_scheme": "fed_avg"})
+    np.random.seed(seed)
+    agg.aggregate_grads([_Client(i, g, Compression(CFGS[name])) for i, g in enumerate(grads)])
+    assert int(np.random.randint(0, 2 ** 31 - 1)) == nxt
+    assert agg.agg_path == "dense-fold"
+    assert agg.agg_grad.dtype == np.float32
+    assert agg.agg_grad.tobytes() == want.tobytes()
