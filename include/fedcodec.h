@@ -321,6 +321,47 @@ int fc_weighted_sum_dense_f64(const void* const* rows, int rows_f64, const doubl
                               uint64_t n, double* out, int continue_sum, fc_stream_t stream);
 int fc_div_scalar_f64(double* x, uint64_t n, double d, fc_stream_t stream);
 
+/* ---- NumPy's legacy MT19937 stream on the device: the reference's own dropout draws ---------
+ * Replaces np.random.binomial(1, p, (n,)) of compression.py:51 / :58 (the process-global legacy
+ * RandomState; NumPy's random_binomial_inversion for n = 1: U = random_sample() from two
+ * 32-bit outputs, kept iff U > exp(log(1 - p)), complemented for p > 0.5).  A round draws the
+ * masks of `rows` consecutive dropout rows of length n, row r starting 2 r n outputs after the
+ * state (key, pos) of np.random.get_state(); the mask words equal
+ * bitmask_words(np.random.binomial(1, p, (n,)), n, True) bit for bit, and the state block
+ * holds the state np.random would be left in (openmsftl_amd/csrc/fc_mt.hip; pinned against
+ * NumPy in tests/test_mt19937.py).
+ *   fc_mt_plan: the jump polynomials of length n for up to `rows` rows (computed on the host,
+ *     cached per n; the first n costs ~0.1-0.5 s) copied into the DEVICE buffer `plan`
+ *     (fc_mt_plan_bytes); synchronises `stream`.  Reusable for every round of length n and
+ *     at most `rows` rows.
+ *   fc_mt_begin: the round's starting state (key: HOST uint32[624], pos in [0, 624]) into
+ *     the DEVICE workspace (fc_mt_workspace_bytes(rows), 256-B aligned), each row's window
+ *     and raw sequence, and the state after `rows` rows into the fc_mt_state at ws offset 0.
+ *   fc_mt_binomial: row `row`'s mask (mask_bits: DEVICE uint32[ceil(n/32)], bits >= n zero),
+ *     after fc_mt_begin on the same stream.  p outside [0, 1] is FC_ERR_ARG (NumPy raises
+ *     ValueError).  NumPy's rare redraw (U - qn > p qn / (1 - p) after U > qn, ~2^-52 per
+ *     element) is not reproduced: fc_mt_state.redraw becomes non-zero and the caller must draw
+ *     the round on the host instead.
+ *   fc_mt_jump_poly / fc_mt_charpoly (HOST, no GPU): z^d mod chi and chi (MT19937's
+ *     characteristic polynomial, degree 19937) as 624 little-endian words (bit i = z^i). */
+#define FC_MT_SEG 32768           /* mask elements per generator wave */
+typedef struct {
+  uint32_t key[624];              /* np.random.get_state()[1] after the round */
+  uint32_t pos;                   /* ... [2] */
+  uint32_t redraw;                /* != 0: NumPy would have redrawn: use host draws */
+  uint32_t rows;
+  uint32_t start_pos;
+} fc_mt_state;
+size_t fc_mt_plan_bytes(uint64_t n, int rows);
+size_t fc_mt_workspace_bytes(int rows);
+int fc_mt_plan(uint64_t n, int rows, void* plan, size_t plan_bytes, fc_stream_t stream);
+int fc_mt_begin(const void* plan, size_t plan_bytes, uint64_t n, int rows, const uint32_t* key,
+                uint32_t pos, void* ws, size_t ws_bytes, fc_stream_t stream);
+int fc_mt_binomial(const void* plan, size_t plan_bytes, uint64_t n, int rows, int row, double p,
+                   uint32_t* mask_bits, void* ws, size_t ws_bytes, fc_stream_t stream);
+int fc_mt_jump_poly(uint64_t d, uint32_t* out_words);
+int fc_mt_charpoly(uint32_t* out_words);
+
 /* ---- measurement: HIP events around selected kernels, on the stream they run on -------
  * mask: FC_TIME_* bits.  Between fc_timing_begin and fc_timing_end every launch of a
  * selected kernel class is bracketed by a hipEvent pair; fc_timing_end synchronises those

@@ -102,6 +102,13 @@ SIGNATURES = {
     "fc_mask_dense_f32": (_i32, [_vp, _u64, _i32, _vp, _dbl, _u64, _u64, _vp, _vp]),
     "fc_weighted_sum_dense_f64": (_i32, [_vp, _i32, _vp, _i32, _u64, _vp, _i32, _vp]),
     "fc_div_scalar_f64": (_i32, [_vp, _u64, _dbl, _vp]),
+    "fc_mt_plan_bytes": (_sz, [_u64, _i32]),
+    "fc_mt_workspace_bytes": (_sz, [_i32]),
+    "fc_mt_plan": (_i32, [_u64, _i32, _vp, _sz, _vp]),
+    "fc_mt_begin": (_i32, [_vp, _sz, _u64, _i32, _vp, ctypes.c_uint32, _vp, _sz, _vp]),
+    "fc_mt_binomial": (_i32, [_vp, _sz, _u64, _i32, _i32, _dbl, _vp, _vp, _sz, _vp]),
+    "fc_mt_jump_poly": (_i32, [_u64, _vp]),
+    "fc_mt_charpoly": (_i32, [_vp]),
     "fc_timing_begin": (_i32, [ctypes.c_uint32]),
     "fc_timing_end": (_i32, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)]),
 }

@@ -48,7 +48,7 @@ from . import _lib as L
 from . import codec
 from .compression import Compression, bitmask_words, kept_count
 from .gar import FedAvg
-from .pipeline import HostFedAvg, RowCodec, RowPlan
+from .pipeline import HostFedAvg, MtRedraw, RowCodec, RowPlan
 
 
 def _cluster_bounds(m: int, cluster_size: int):
@@ -143,7 +143,33 @@ def _streamable(C, n: int) -> bool:
     return rng == "numpy" or 0.0 <= p <= 1.0
 
 
-def row_plan(clients, n: int) -> Optional[RowPlan]:
+#: draw the reference's np.random dropout masks on the device (np.random's MT19937 stream by
+#: jump-ahead, openmsftl_amd/csrc/fc_mt.hip) instead of on the host producer thread
+DEVICE_MT = True
+
+
+def _device_mt_ok(clients) -> bool:
+    """Can the round's np.random draws be made on the device?  Only if every host-RNG row is a
+    dropout row with p in [0, 1]: 'rand' (np.random.permutation) consumes a data-dependent
+    number of draws, and an invalid p must raise at its row (the host path does)."""
+    for c in clients:
+        C = c.C
+        fn = C.compression_function
+        if getattr(C, "rng", "numpy") != "numpy":
+            continue
+        if fn == "rand":
+            return False
+        if fn in ("dropout-biased", "dropout-unbiased"):
+            try:
+                p = float(C.dropout_p)
+            except (TypeError, ValueError):
+                return False
+            if not 0.0 <= p <= 1.0:
+                return False
+    return True
+
+
+def row_plan(clients, n: int, device_mt: Optional[bool] = None) -> Optional[RowPlan]:
     """The streamed round's :class:`~openmsftl_amd.pipeline.RowPlan` (aggregation.py:61-63:
     row ix = compress(clients[ix].grad)), or None when some client's codec cannot stream.
 
@@ -155,9 +181,14 @@ def row_plan(clients, n: int) -> Optional[RowPlan]:
       Bernoulli(p) (Philox); the unbiased 1/p scaling is applied by the fold
       (fl32(fl64(g) / p), compression.py:59-60 then the cast into G, aggregation.py:63).
     Host draws run in row order on the plan's producer thread, exactly the reference's
-    consumption of the global RNG; Philox offsets are taken in row order too."""
+    consumption of the global RNG; Philox offsets are taken in row order too.  With
+    ``device_mt`` (default :data:`DEVICE_MT`) and no host permutation in the round, the dropout
+    masks are np.random's own draws made on the device instead (mask_src "mt": row r of the
+    round's MtRound, from np.random's state now; :meth:`RowPlan.close` sets the state after)."""
     if not all(_streamable(c.C, n) for c in clients):
         return None
+    use_mt = (DEVICE_MT if device_mt is None else device_mt) and _device_mt_ok(clients)
+    mt_rows = 0
     specs, draws = [], {}
     for i, c in enumerate(clients):
         C = c.C
@@ -184,13 +215,16 @@ def row_plan(clients, n: int) -> Optional[RowPlan]:
             continue
         cid = L.FC_CODEC_DROPOUT_BIASED if fn == "dropout-biased" else L.FC_CODEC_DROPOUT_UNBIASED
         p = float(C.dropout_p)
-        if rng == "numpy":
+        if rng == "numpy" and use_mt:
+            specs.append(RowCodec("mask", codec=cid, p=p, mask_src="mt", offset=mt_rows))
+            mt_rows += 1
+        elif rng == "numpy":
             specs.append(RowCodec("mask", codec=cid, p=p, mask_src="host"))
             draws[i] = (lambda p=C.dropout_p: bitmask_words(np.random.binomial(1, p, (n,)), n, True))
         else:
             specs.append(RowCodec("mask", codec=cid, p=p, mask_src="philox", seed=C.seed,
                                   offset=C._next_offset()))
-    return RowPlan(n, specs, draws)
+    return RowPlan(n, specs, draws, mt_rows=mt_rows)
 
 
 #: device bytes the streamed path may hold (gradient ring + packets + aggregates);
@@ -331,25 +365,33 @@ def aggregate_grads(self, clients: List, input_feature: np.ndarray = None,
     # (RandomGaussian Byzantine noise, attack_models.py:105-118) is compressed in its own dtype
     # and cast into G's float32 row by the generic path, as aggregation.py:63 does
     all_f32 = all(np.asarray(c.grad).dtype == np.float32 for c in clients)
-    if device_gar and all_f32 and f32_weights and n > 0:
+    streamable = device_gar and all_f32 and f32_weights and n > 0
+    if streamable:
         plan = row_plan(clients, n)
     if plan is not None:
         # streamed from the host gradients, G never built (rows live group by group)
         self.agg_path = "stream"
-        try:
-            if self.num_hierarchies > 0:
-                H = merge_streamed(self, clients, n, plan, self.cluster_size_list[0], dev)
-                H = merge_stages(H, self.cluster_size_list[1:])
-                self.curr_G = H
-                agg = self.gar.aggregate(G=H, client_ids=np.arange(H.shape[0]))
-            else:
-                self.curr_G = None
-                w = self.gar._weights(len(clients), np.float32)     # gar.py:37-42 (persisted)
-                agg = stream_fold(self, clients, n, plan, w, dev)
-        except BaseException:
-            plan.close(wait=False)
-            raise
-        plan.close()                        # every host draw done: the RNG is where the reference leaves it
+        while True:
+            try:
+                if self.num_hierarchies > 0:
+                    H = merge_streamed(self, clients, n, plan, self.cluster_size_list[0], dev)
+                    H = merge_stages(H, self.cluster_size_list[1:])
+                    self.curr_G = H
+                    agg = self.gar.aggregate(G=H, client_ids=np.arange(H.shape[0]))
+                else:
+                    self.curr_G = None
+                    w = self.gar._weights(len(clients), np.float32)     # gar.py:37-42 (persisted)
+                    agg = stream_fold(self, clients, n, plan, w, dev)
+            except BaseException:
+                plan.close(wait=False)
+                raise
+            try:
+                plan.close()                # every draw done: the RNG is where the reference leaves it
+            except MtRedraw:                # NumPy would redraw somewhere (~2^-52 per element):
+                plan = row_plan(clients, n, device_mt=False)   # the reference's host draws
+                continue
+            break
+        self.agg_draws = "device-mt" if plan.mt_rows else ("host" if plan.draws else None)
     else:
         # generic codec mix / float64: the drop-in Compression per client, in row order; rows
         # take G's dtype (aggregation.py:61-63: G = zeros(..., dtype=clients[0].grad.dtype))
@@ -398,6 +440,7 @@ class Aggregator:
         self.curr_G = None
         self.agg_grad = None
         self.agg_path = None                # "stream" | "dense-fold" | "dense": the last call's path
+        self.agg_draws = None               # streamed np.random draws: "device-mt" | "host" | None
         self.analyze_pc = self.aggregation_config.get("pc_analysis", False)
         self.num_hierarchies = self.aggregation_config.get("num_hierarchies", 0)
         self.cluster_size_list = self.aggregation_config.get("cluster_size_list", [])

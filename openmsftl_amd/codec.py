@@ -850,3 +850,99 @@ def decode_accumulate_qsgd(packets: Sequence[QsgdPacket], weights, out: Optional
                                           int(continue_sum), _stream(dev)),
             "fc_qsgd_decode_accumulate")
     return out
+
+
+# ---- NumPy's legacy MT19937 stream on the device (the reference's dropout draws) -------------
+class MtPlan:
+    """The jump polynomials of gradient length n on one device (fc_mt_plan), for up to
+    ``rows`` rows per round; kept per (device, n) and grown on demand."""
+
+    _cache: dict = {}
+    _lock = threading.Lock()
+
+    def __init__(self, n: int, rows: int, device: torch.device):
+        lib = L.load()
+        self.n, self.rows = n, rows
+        self.nbytes = int(lib.fc_mt_plan_bytes(n, rows))
+        self.buf = torch.empty(self.nbytes, dtype=torch.uint8, device=device)
+        L.check(lib.fc_mt_plan(n, rows, _vp(self.buf), self.nbytes, _stream(device)), "fc_mt_plan")
+
+    @classmethod
+    def get(cls, n: int, rows: int, device: torch.device) -> "MtPlan":
+        key = (device.index if device.index is not None else torch.cuda.current_device(), n)
+        with cls._lock:
+            p = cls._cache.get(key)
+            if p is None or p.rows < rows:
+                p = cls(n, max(rows, 2 * p.rows if p is not None else rows), device)
+                cls._cache[key] = p
+            return p
+
+
+class MtRound:
+    """``rows`` consecutive ``np.random.binomial(1, p_r, (n,))`` draws (compression.py:51, :58)
+    generated on the device from the legacy state (key, pos) of ``np.random.get_state()``
+    (fc_mt_begin / fc_mt_binomial): row r's mask words equal the host draw's
+    ``bitmask_words(mask, n, True)``.  :meth:`end_state` gives the state np.random is left in
+    (and whether NumPy would have redrawn somewhere: the caller then draws on the host)."""
+
+    def __init__(self, n: int, rows: int, key: np.ndarray, pos: int,
+                 device: Optional[torch.device] = None):
+        dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        lib = L.load()
+        self.n, self.rows, self.dev = n, rows, dev
+        self.plan = MtPlan.get(n, rows, dev)
+        self.nbytes = int(lib.fc_mt_workspace_bytes(rows))
+        self.ws = torch.empty(self.nbytes, dtype=torch.uint8, device=dev)
+        self._key = np.ascontiguousarray(np.asarray(key, dtype=np.uint32))
+        if self._key.shape != (624,):
+            raise ValueError("an MT19937 key has 624 words")
+        with torch.cuda.device(dev):
+            L.check(lib.fc_mt_begin(_vp(self.plan.buf), self.plan.nbytes, n, rows,
+                                    self._key.ctypes.data_as(ctypes.c_void_p), int(pos),
+                                    _vp(self.ws), self.nbytes, _stream(dev)), "fc_mt_begin")
+        self._events = []                   # after begin and each row: end_state() waits on them
+        self._mark()
+        self._begin = (self._events[0], torch.cuda.current_stream(dev))
+
+    def _mark(self) -> None:
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.dev))
+        self._events.append(ev)
+        if len(self._events) > 8:
+            self._events = [e for e in self._events if not e.query()] or self._events[-1:]
+
+    def binomial(self, row: int, p: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Row ``row``'s mask as int32 bit words (ceil(n/32)) on the current stream."""
+        if out is None:
+            out = torch.empty((self.n + 31) // 32, dtype=torch.int32, device=self.dev)
+        cur = torch.cuda.current_stream(self.dev)
+        if cur != self._begin[1]:           # rows may be drawn on other streams (DeviceRing)
+            cur.wait_event(self._begin[0])
+        lib = L.load()
+        L.check(lib.fc_mt_binomial(_vp(self.plan.buf), self.plan.nbytes, self.n, self.rows, int(row),
+                                   float(p), _vp(out), _vp(self.ws), self.nbytes,
+                                   _stream(self.dev)), "fc_mt_binomial")
+        self._mark()
+        return out
+
+    def end_state(self):
+        """(key uint32[624], pos, redraw) after the round: waits for begin and every row
+        launched so far (the redraw flag covers those rows)."""
+        for ev in self._events:
+            ev.synchronize()
+        raw = self.ws[:624 * 4 + 16].cpu().numpy()
+        words = raw.view(np.uint32)
+        return words[:624].copy(), int(words[624]), bool(words[625])
+
+
+def mt_state():
+    """np.random's legacy state as (key, pos, has_gauss, gauss); ValueError if not MT19937."""
+    st = np.random.get_state()
+    if st[0] != "MT19937":
+        raise ValueError("np.random is not an MT19937 RandomState")
+    return np.asarray(st[1], dtype=np.uint32), int(st[2]), int(st[3]), float(st[4])
+
+
+def mt_set_state(key: np.ndarray, pos: int, has_gauss: int, gauss: float) -> None:
+    np.random.set_state(("MT19937", np.asarray(key, dtype=np.uint32), int(pos), int(has_gauss),
+                         float(gauss)))

@@ -6,3 +6,4 @@
 #include "fc_qsgd.hip"
 #include "fc_f64.hip"
 #include "fc_capi.hip"
+#include "fc_mt.hip"

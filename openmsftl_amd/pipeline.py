@@ -94,8 +94,10 @@ class RowCodec:
     kind "top": fc_topk_encode packet of the k largest keys (``key_mode`` MAGNITUDE = 'top',
     PHILOX = native 'rand' keyed by ``seed``/``offset``); "mask": fc_mask_encode idx/val packet
     of codec ``codec`` (FC_CODEC_RAND / DROPOUT_*) with ``mask_src`` "host" (bits drawn on the
-    host, :meth:`RowPlan.take_mask`), "philox" (device Bernoulli(p)) or "none" (nothing kept:
-    'top' with k = 0); "dense": the gradient itself ('full', or 'top' with k = n)."""
+    host, :meth:`RowPlan.take_mask`), "mt" (np.random.binomial's own MT19937 draws made on the
+    device, row ``offset`` of the plan's :class:`~openmsftl_amd.codec.MtRound`), "philox"
+    (device Bernoulli(p)) or "none" (nothing kept: 'top' with k = 0); "dense": the gradient
+    itself ('full', or 'top' with k = n)."""
     kind: str
     k: int = 0
     key_mode: int = 0
@@ -104,6 +106,12 @@ class RowCodec:
     codec: int = 0
     p: float = 0.0
     mask_src: str = "none"
+
+
+class MtRedraw(RuntimeError):
+    """NumPy's binomial would have redrawn a variate (probability ~2^-52 per element) in a
+    device MT19937 round: its masks from that element on are not the reference's; redo the
+    round with host draws (np.random is still at the round's start)."""
 
 
 class RowPlan:
@@ -118,11 +126,19 @@ class RowPlan:
     reference leaves it) and re-raises a draw's exception (e.g. NumPy's ValueError for p > 1)."""
 
     def __init__(self, n: int, specs: Sequence[RowCodec], draws: Optional[dict] = None,
-                 lookahead: int = 8, base: int = 0, parent: "RowPlan" = None):
+                 lookahead: int = 8, base: int = 0, parent: "RowPlan" = None,
+                 mt_rows: int = 0):
         self.n, self.specs, self.base = n, specs, base
         self._root = parent if parent is not None else self
         if parent is not None:
             return
+        # device MT19937 rows ("mt"): the round's start state is np.random's now; close() leaves
+        # np.random where the reference's loop would (the state after mt_rows binomial draws)
+        self.mt_rows = mt_rows
+        self._mt_start = codec.mt_state() if mt_rows else None
+        self._mt_rounds = {}
+        self._mt_lock = threading.Lock()
+        self._mt_redraw = False
         self.draws = dict(draws or {})
         self.nwords = (n + 31) // 32
         self._cv = threading.Condition()
@@ -227,7 +243,9 @@ class RowPlan:
             r._cv.notify_all()
 
     def close(self, wait: bool = True) -> None:
-        """wait=True: every draw has run (raises the first draw error); False: stop early."""
+        """wait=True: every draw has run (raises the first draw error; a device MT round
+        sets np.random to the state after its draws, or raises :class:`MtRedraw`); False:
+        stop early (np.random keeps the state it had when the plan was made)."""
         r = self._root
         if wait:
             r._start()
@@ -240,6 +258,36 @@ class RowPlan:
             r._thread = None
         if wait and r._err is not None:
             raise r._err[1]
+        if wait and r.mt_rows:
+            r._mt_finish()
+
+    # ---- device MT19937 rows --------------------------------------------------------------
+    def mt_round(self, dev: torch.device) -> "codec.MtRound":
+        """The round's :class:`~openmsftl_amd.codec.MtRound` on ``dev`` (begun on the current
+        stream the first time a pipeline of that device asks)."""
+        r = self._root
+        key = dev.index if dev.index is not None else torch.cuda.current_device()
+        with r._mt_lock:
+            R = r._mt_rounds.get(key)
+            if R is None:
+                k, pos, _, _ = r._mt_start
+                R = codec.MtRound(r.n, r.mt_rows, k, pos, dev)
+                r._mt_rounds[key] = R
+            return R
+
+    def mt_redraw_seen(self) -> bool:
+        """Did a row drawn so far on any device hit NumPy's redraw (synchronises)?"""
+        return any(R.end_state()[2] for R in list(self._root._mt_rounds.values()))
+
+    def _mt_finish(self) -> None:
+        rounds = list(self._mt_rounds.values()) or [self.mt_round(
+            torch.device("cuda", torch.cuda.current_device()))]
+        ends = [R.end_state() for R in rounds]          # synchronises
+        if self._mt_redraw or any(e[2] for e in ends):
+            raise MtRedraw("NumPy would redraw a binomial variate in this round")
+        key, pos, _ = ends[0]
+        _, _, has_gauss, gauss = self._mt_start
+        codec.mt_set_state(key, pos, has_gauss, gauss)
 
 
 def top_plan(n: int, k: int, clients: int) -> RowPlan:
@@ -393,13 +441,17 @@ class HostFedAvg:
         if done is not None:
             done.record(self.copy)
 
-    def _mask_slot(self, slot: int, plan: RowPlan, i: int) -> torch.Tensor:
-        """Row i's host-drawn mask into the ring slot's device mask words (copy stream, after
-        the slot's previous encode: queue it after :meth:`_h2d` of the same slot)."""
+    def _mslot(self, slot: int) -> torch.Tensor:
         if self.mslots is None:
             words = (self.n + 31) // 32
             self.mslots = [torch.empty(words, dtype=torch.int32, device=self.dev)
                            for _ in range(self.ring)]
+        return self.mslots[slot]
+
+    def _mask_slot(self, slot: int, plan: RowPlan, i: int) -> torch.Tensor:
+        """Row i's host-drawn mask into the ring slot's device mask words (copy stream, after
+        the slot's previous encode: queue it after :meth:`_h2d` of the same slot)."""
+        self._mslot(slot)
         buf = plan.take_mask(i)
         with torch.cuda.stream(self.copy):
             self.mslots[slot].copy_(buf, non_blocking=True)
@@ -463,6 +515,10 @@ class HostFedAvg:
             self._h2d(get(i), self.slots[s], wait=self.enc_done[s])
             mask = self._mask_slot(s, plan, i) if rc.mask_src == "host" else None
             self.h2d_done[s].record(self.copy)
+            if rc.mask_src == "mt":                 # np.random.binomial's draws, on the device,
+                # made while the row's gradient is still on its way (the slot's previous
+                # encode, its last reader, is earlier on this stream)
+                mask = plan.mt_round(self.dev).binomial(rc.offset, rc.p, out=self._mslot(s))
             comp.wait_event(self.h2d_done[s])
             if rc.kind == "top":
                 codec.encode_top(self.slots[s], rc.k, key_mode=rc.key_mode, seed=rc.seed,
@@ -817,4 +873,14 @@ class RankRing:
             with torch.cuda.device(self.pipe.dev), torch.cuda.stream(self.fold):
                 self._recv(acc, last_owner)
         cur.wait_stream(self.fold)
+        root = plan._root
+        if root.mt_rows and W > 1:
+            # a redraw seen by one rank must send every rank to the host draws (MtRedraw at
+            # close), or the ranks would leave np.random in different states
+            import torch.distributed as dist
+            flag = torch.tensor([int(root.mt_redraw_seen())], dtype=torch.int32)
+            if not self._gloo():
+                flag = flag.to(self.pipe.dev)
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.pg)
+            root._mt_redraw = bool(int(flag.item()))
         return acc if r == self.dst else None

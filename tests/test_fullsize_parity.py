@@ -150,15 +150,17 @@ def test_configs4_device_aggregator_70x25M(configs4_host, pin):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("codec_name,clients", [("full", 70), ("dropout-unbiased", 16),
-                                                ("rand", 6)])
+@pytest.mark.parametrize("codec_name,clients", [("full", 70), ("dropout-unbiased", 32),
+                                                ("dropout-biased", 16), ("rand", 6)])
 def test_configs4_device_aggregator_other_codecs(configs4_host, codec_name, clients):
     """The Aggregator's streamed path for the other codecs at the configs[4] size (25.5 M):
     'full' (the reference's configured codec, client_config.json:48) over all 70 clients,
-    'dropout-unbiased' p = 0.1 and 'rand' f = 0.01 (host masks drawn from np.random in row
-    order) over the first clients, with the default device budget; agg_grad byte-equal to the
-    oracle's row-order fold of the oracle's rows (compression.py:39-60, gar.py:44) and the
-    RNG where the reference leaves it.  Prints the NumPy-to-NumPy rate."""
+    'dropout-*' p = 0.1 (np.random.binomial's own MT19937 draws made on the device,
+    openmsftl_amd/csrc/fc_mt.hip) and 'rand' f = 0.01 (host permutation masks drawn from
+    np.random in row order) over the first clients, with the default device budget; agg_grad
+    byte-equal to the oracle's row-order fold of the oracle's rows (compression.py:39-60,
+    gar.py:44) and the RNG where the reference leaves it.  Prints the NumPy-to-NumPy rate
+    (DESIGN.md §5)."""
     import time
 
     from oracle import compression_oracle as co
@@ -179,6 +181,7 @@ def test_configs4_device_aggregator_other_codecs(configs4_host, codec_name, clie
         agg.aggregate_grads([_Client(i, g, C) for i, g in enumerate(grads)])
         dt = time.perf_counter() - t0
         assert agg.agg_path == "stream"
+        assert agg.agg_draws == {"full": None, "rand": "host"}.get(codec_name, "device-mt")
         assert int(np.random.randint(0, 2 ** 31 - 1)) == nxt
         assert agg.agg_grad.tobytes() == want.tobytes(), f"{codec_name}: aggregate differs"
     gbps = 4.0 * D["configs4"]["n"] * clients / dt / 1e9

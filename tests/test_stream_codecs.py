@@ -150,7 +150,7 @@ def test_row_plan_restrict_and_shift():
     from openmsftl_amd.compression import bitmask_words
     np.random.seed(seed)
     C = Compression({"compression_function": "dropout-biased", "dropout_p": 0.3})
-    plan = row_plan([_Client(i, np.zeros(n, np.float32), C) for i in range(9)], n)
+    plan = row_plan([_Client(i, np.zeros(n, np.float32), C) for i in range(9)], n, device_mt=False)
     plan.restrict(lambda i: i % 3 == 1)
     sub = plan.shifted(4)
     for i in (1, 4, 7):
@@ -191,12 +191,19 @@ def _budget(n, packets, sets=1):
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", list(CFGS))
 @pytest.mark.parametrize("ref_objects", [False, True])
-def test_aggregator_streams_every_codec(name, ref_objects):
+@pytest.mark.parametrize("device_mt", [True, False])
+def test_aggregator_streams_every_codec(name, ref_objects, device_mt, monkeypatch):
     """agg_grad byte-equal to the reference round (oracle), M x N far above the device budget
-    (3 packets per fold group: 6 groups), the RNG state after the round equal."""
+    (3 packets per fold group: 6 groups), the RNG state after the round equal — with the
+    dropout masks drawn on the device (np.random's MT19937 stream, the default) and on the
+    host (the reference's own np.random.binomial calls)."""
     pytest.importorskip("torch")
     from openmsftl_amd import Compression
+    from openmsftl_amd import aggregation
     from openmsftl_amd.aggregation import Aggregator
+    if not device_mt and not name.startswith("dropout"):
+        pytest.skip("only dropout rows draw on the device")
+    monkeypatch.setattr(aggregation, "DEVICE_MT", device_mt)
     grads = _grads(M, N, seed=sorted(CFGS).index(name))
     seed = 31
     want, nxt = _reference_round([CFGS[name]] * M, grads, seed)
@@ -208,6 +215,8 @@ def test_aggregator_streams_every_codec(name, ref_objects):
     agg.aggregate_grads([_Client(i, g, mk(CFGS[name])) for i, g in enumerate(grads)])
     assert int(np.random.randint(0, 2 ** 31 - 1)) == nxt
     assert agg.agg_path == "stream" and agg.curr_G is None
+    if name.startswith("dropout"):
+        assert agg.agg_draws == ("device-mt" if device_mt else "host")
     (pipe,) = agg._host_pipelines.values()
     assert pipe.group == 3
     assert agg.agg_grad.dtype == np.float32
@@ -387,4 +396,82 @@ def test_aggregator_mixed_dtype_round_takes_the_generic_path(name):
     assert int(np.random.randint(0, 2 ** 31 - 1)) == nxt
     assert agg.agg_path == "dense-fold"
     assert agg.agg_grad.dtype == np.float32
+    assert agg.agg_grad.tobytes() == want.tobytes()
+
+
+def test_row_plan_draws_dropout_on_the_device_when_it_can():
+    """No host permutation in the round and every p in [0, 1]: the dropout rows become device
+    MT19937 rows (mask_src "mt", numbered in row order) and nothing is drawn on the host; a
+    'rand' (numpy) row or an invalid p keeps the host draws."""
+    from openmsftl_amd import Compression
+    from openmsftl_amd.aggregation import row_plan
+    n = 1000
+    names = ["dropout-biased", "top", "full", "dropout-unbiased", "dropout-biased"]
+    clients = [_Client(i, np.zeros(n, np.float32), Compression(CFGS[x])) for i, x in enumerate(names)]
+    state = np.random.get_state()[1].copy()
+    plan = row_plan(clients, n)
+    assert [(r.kind, r.mask_src, r.offset) for r in plan.specs] == [
+        ("mask", "mt", 0), ("top", "none", 0), ("dense", "none", 0), ("mask", "mt", 1),
+        ("mask", "mt", 2)]
+    assert plan.mt_rows == 3 and not plan.draws
+    assert (np.random.get_state()[1] == state).all()
+    plan.close(wait=False)
+    clients.append(_Client(5, np.zeros(n, np.float32), Compression(CFGS["rand"])))
+    plan = row_plan(clients, n)
+    assert plan.mt_rows == 0 and sorted(plan.draws) == [0, 3, 4, 5]
+    plan.close(wait=False)
+    bad = [_Client(0, np.zeros(n, np.float32), _RefCompression({"compression_function":
+                                                                  "dropout-biased", "dropout_p": float("nan")}))]
+    plan = row_plan(bad, n)
+    assert plan.mt_rows == 0 and sorted(plan.draws) == [0]
+    plan.close(wait=False)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sizes", [[], [3], [4, 2]])
+def test_aggregator_device_mt_with_other_codecs_and_merges(sizes):
+    """Dropout rows (device MT19937 draws) among 'top' / 'full' rows, with hierarchical merges
+    over the streamed rows (shifted plans): byte-equal to the reference round, RNG equal."""
+    pytest.importorskip("torch")
+    from openmsftl_amd import Compression
+    from openmsftl_amd.aggregation import Aggregator
+    names = ["dropout-unbiased", "top", "full", "dropout-biased", "dropout-unbiased", "top",
+             "dropout-biased", "full", "dropout-unbiased", "dropout-unbiased", "top"]
+    cfgs = [dict(CFGS[x]) for x in names]
+    cfgs[3]["dropout_p"] = 0.7                          # p > 0.5: the complemented draw
+    cfgs[8]["dropout_p"] = 1.0                          # everything kept
+    cfgs[9] = {"compression_function": "dropout-biased", "dropout_p": 0.0}   # nothing kept
+    grads = _grads(len(cfgs), N, seed=91)
+    seed = 77
+    with np.errstate(divide="ignore", invalid="ignore"):
+        want, nxt = _reference_round(cfgs, grads, seed, sizes)
+    agg = Aggregator({"aggregation_scheme": "fed_avg", "device_budget_bytes": _budget(N, 3),
+                      "num_hierarchies": len(sizes), "cluster_size_list": sizes})
+    np.random.seed(seed)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        agg.aggregate_grads([_Client(i, g, Compression(c)) for i, (g, c) in enumerate(zip(grads, cfgs))])
+    assert int(np.random.randint(0, 2 ** 31 - 1)) == nxt
+    assert agg.agg_path == "stream" and agg.agg_draws == "device-mt"
+    nan = np.isnan(want)
+    np.testing.assert_array_equal(np.isnan(agg.agg_grad), nan)
+    assert agg.agg_grad[~nan].tobytes() == want[~nan].tobytes()
+
+
+@pytest.mark.gpu
+def test_aggregator_device_mt_redraw_falls_back_to_host_draws(monkeypatch):
+    """NumPy's binomial redraw (~2^-52 per element) cannot be reproduced by the device stream:
+    when a round reports one, the round is redone with the host draws from the same start state
+    — here forced by a device round that claims a redraw."""
+    pytest.importorskip("torch")
+    from openmsftl_amd import Compression, codec
+    from openmsftl_amd.aggregation import Aggregator
+    real = codec.MtRound.end_state
+    monkeypatch.setattr(codec.MtRound, "end_state", lambda self: real(self)[:2] + (True,))
+    grads = _grads(6, N, seed=12)
+    want, nxt = _reference_round([CFGS["dropout-unbiased"]] * 6, grads, 5)
+    agg = Aggregator({"aggregation_scheme": "fed_avg"})
+    np.random.seed(5)
+    agg.aggregate_grads([_Client(i, g, Compression(CFGS["dropout-unbiased"])) for i, g in enumerate(grads)])
+    assert agg.agg_draws == "host"
+    assert int(np.random.randint(0, 2 ** 31 - 1)) == nxt
     assert agg.agg_grad.tobytes() == want.tobytes()
