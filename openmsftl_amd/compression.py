@@ -10,8 +10,10 @@ Same constructor keys and defaults, same ``compress(grad, layer_wise=False)`` co
 The compute runs in hand-written HIP kernels (libfedcodec.so); there is no CPU fallback.
 
 RNG: by default ('rng': 'numpy') 'rand'/'dropout-*' draw from the process-global legacy
-``np.random`` exactly as the reference (same calls, same stream consumption), and only the
-mask/index set crosses to the GPU.  ``'rng': 'philox'`` draws on the device instead
+``np.random`` exactly as the reference (same stream consumption, same state afterwards):
+'rand' calls ``np.random.permutation`` and only the index set crosses to the GPU; 'dropout-*'
+generates ``np.random.binomial``'s own MT19937 variates on the device (jump-ahead from
+``np.random.get_state()``, openmsftl_amd/csrc/fc_mt.hip) and sets the state after them.  ``'rng': 'philox'`` draws on the device instead
 (Philox4x32-10 keyed by ``'seed'``, counter advanced per call) — no host RNG work, not
 stream-identical to the reference (documented in DESIGN.md).
 
@@ -36,6 +38,19 @@ import torch
 
 from . import _lib as L
 from . import codec
+
+
+#: 'dropout-*' with the numpy RNG: draw np.random.binomial's MT19937 variates on the device
+#: (bit-exact, RNG state included; openmsftl_amd/csrc/fc_mt.hip) instead of calling it
+DEVICE_MT = True
+
+
+def _valid_p(p) -> bool:
+    """p the device draws accept: a real number in [0, 1] (NumPy raises for the rest)."""
+    try:
+        return 0.0 <= float(p) <= 1.0
+    except (TypeError, ValueError):
+        return False
 
 
 def kept_count(fraction: float, n: int) -> int:
@@ -117,8 +132,22 @@ class Compression:
             return out if on_device else out.cpu().numpy()
         # dropout-* ---------------------------------------------------------------------
         p = self.dropout_p
+        codec_id = L.FC_CODEC_DROPOUT_BIASED if fn == 'dropout-biased' else L.FC_CODEC_DROPOUT_UNBIASED
         host_mask = None
         if self.rng == 'numpy':
+            if n > 0 and DEVICE_MT and _valid_p(p):
+                # np.random.binomial(1, p, (n,))'s own MT19937 draws, made on the device
+                # (fc_mt.hip), np.random left where the call leaves it
+                g = self._to_device(grad)
+                key, pos, has_gauss, gauss = codec.mt_state()
+                R = codec.MtRound(n, 1, key, pos, g.device)
+                out = codec.mask_dense_f64(g, codec_id, p=float(p), mask_bits=R.binomial(0, float(p)))
+                key, pos, redraw = R.end_state()
+                if not redraw:
+                    codec.mt_set_state(key, pos, has_gauss, gauss)
+                    return out if on_device else out.cpu().numpy()
+                # NumPy would redraw one variate (~2^-52 per element): its own call below,
+                # from the same (untouched) state
             host_mask = np.random.binomial(1, p, (n,))            # compression.py:51/58
         elif not (0.0 <= p <= 1.0):
             raise ValueError("p < 0, p > 1 or p is NaN")
@@ -126,7 +155,6 @@ class Compression:
             return (torch.zeros(0, dtype=torch.float64, device=grad.device) if on_device
                     else np.zeros(0, dtype=np.float64))
         g = self._to_device(grad)
-        codec_id = L.FC_CODEC_DROPOUT_BIASED if fn == 'dropout-biased' else L.FC_CODEC_DROPOUT_UNBIASED
         # the dense float64 q = g * mask (/ p) the reference returns, float32 g promoted
         # exactly (-0.0 for dropped negative g, NaN for dropped inf/NaN); the packet form of
         # these codecs is codec.encode_mask (bitmap + kept values) for device folds
