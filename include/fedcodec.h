@@ -25,15 +25,14 @@
  * thread-local).  Device-side outcomes (e.g. the sampled bracket missing) are reported in the
  * packet header's `status`, read by the host after the stream is synchronised.
  *
- * Concurrency: every entry point may run beside any other kernel, on any stream, with one
- * exception.  fc_topk_encode (key_mode MAGNITUDE, 0 < k < n) and fc_topk_encode_dense launch
- * k_fused_mag, whose compaction workgroups wait in-kernel (bounded) for the bracket its sample
- * workgroups publish; two such launches on two streams of one device can, in principle, stall
- * each other until that bound (~8192 polls, 2-4 ms), and the call then reports
- * FC_STATUS_RETRY_EXACT: correct after the exact re-encode, but late (400 concurrent fused
- * encodes on two streams at 16 M: no stall, tests/test_gpu_parity.py).  Queue those two on one
- * stream, or order them with events, to rule it out (the Python layer does:
- * codec._fused_encode).  The batched, mask, rand-k, float64, exact, decode and fold
+ * Concurrency: every entry point may run beside any other kernel, on any stream.  Two
+ * launches wait in-kernel (bounded) for a bracket their own sample workgroups publish: k_fused_mag
+ * (fc_topk_encode with key_mode MAGNITUDE and 0 < k < n, fc_topk_encode_dense) and k_fused64
+ * (fc_topk_dense_f64_sampled).  Two of them on two streams of one device could stall each other
+ * (each XCD dispatches the two grids in its own order), so the library queues each one after the
+ * device's previous one: an event it owns is recorded after every such launch, and a launch on
+ * another stream first waits for it.  A launch into a stream being captured (hipGraph) is not
+ * ordered; bracket the graph's launch with fc_fused_order_begin / fc_fused_order_end.  All other
  * kernels synchronise only through last-arriver tickets (no workgroup waits for another).
  */
 #ifndef FEDCODEC_H_
@@ -161,6 +160,15 @@ int fc_topk_encode(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_
  * FC_FMT_DENSE (thresh / status valid; not decodable).  If the header reports
  * FC_STATUS_RETRY_EXACT, `dense` is not valid: re-encode with fc_topk_encode_exact (a full
  * packet) and fc_decode_dense.  Needs 0 < k < n. */
+/* fc_topk_encode_decode: the packet encode of fc_topk_encode (key_mode MAGNITUDE, 0 < k < n,
+ * qoff required) AND its dense decode into out (float32[n], 16-B aligned), with the resolve's
+ * gather and finish inside the decode launch (k_fused_mag -> k_beta -> k_decode_res): the packet
+ * (entries, counts, quarter offsets, header with T64) equals fc_topk_encode's byte for byte and
+ * out equals fc_decode_dense of it.  Replaces compression.py:31-37 + the caller's use of q.
+ * Header status FC_STATUS_RETRY_EXACT: call fc_topk_encode_exact, then fc_decode_dense. */
+int fc_topk_encode_decode(const float* g, uint64_t n, uint64_t k, uint16_t* idx, float* val,
+                          uint64_t capacity, uint32_t* cnt, uint64_t* qoff, fc_packet_hdr* hdr,
+                          void* ws, size_t ws_bytes, float* out, fc_stream_t stream);
 int fc_topk_encode_dense(const float* g, uint64_t n, uint64_t k, uint16_t* idx, float* val,
                          uint64_t capacity, uint32_t* cnt, uint64_t* qoff, fc_packet_hdr* hdr,
                          void* ws, size_t ws_bytes, float* dense, fc_stream_t stream);
@@ -361,6 +369,13 @@ int fc_mt_binomial(const void* plan, size_t plan_bytes, uint64_t n, int rows, in
                    uint32_t* mask_bits, void* ws, size_t ws_bytes, fc_stream_t stream);
 int fc_mt_jump_poly(uint64_t d, uint32_t* out_words);
 int fc_mt_charpoly(uint32_t* out_words);
+
+/* Ordering of in-kernel-waiting launches issued outside the library's own calls (a replayed
+ * graph that contains fc_topk_encode / fc_topk_encode_dense / fc_topk_dense_f64_sampled):
+ * fc_fused_order_begin(s) makes s wait for the device's last such launch; fc_fused_order_end(s)
+ * marks s as holding the latest one. */
+int fc_fused_order_begin(fc_stream_t stream);
+int fc_fused_order_end(fc_stream_t stream);
 
 /* ---- measurement: HIP events around selected kernels, on the stream they run on -------
  * mask: FC_TIME_* bits.  Between fc_timing_begin and fc_timing_end every launch of a

@@ -77,6 +77,8 @@ SIGNATURES = {
                               _vp, _vp, _sz, _vp]),
     "fc_topk_encode_dense": (_i32, [_vp, _u64, _u64, _vp, _vp, _u64, _vp, _vp, _vp, _vp, _sz,
                                     _vp, _vp]),
+    "fc_topk_encode_decode": (_i32, [_vp, _u64, _u64, _vp, _vp, _u64, _vp, _vp, _vp, _vp, _sz,
+                                     _vp, _vp]),
     "fc_workspace_bytes_batch": (_sz, [_u64, _i32]),
     "fc_topk_encode_batch": (_i32, [_vp, _i32, _u64, _u64, _i32, _u64, _vp, _sz, _vp]),
     "fc_topk_encode_batch_part": (_i32, [_vp, _i32, _u64, _u64, _i32, _u64, _vp, _sz, _i32, _vp]),
@@ -109,6 +111,8 @@ SIGNATURES = {
     "fc_mt_binomial": (_i32, [_vp, _sz, _u64, _i32, _i32, _dbl, _vp, _vp, _sz, _vp]),
     "fc_mt_jump_poly": (_i32, [_u64, _vp]),
     "fc_mt_charpoly": (_i32, [_vp]),
+    "fc_fused_order_begin": (_i32, [_vp]),
+    "fc_fused_order_end": (_i32, [_vp]),
     "fc_timing_begin": (_i32, [ctypes.c_uint32]),
     "fc_timing_end": (_i32, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)]),
 }

@@ -13,7 +13,6 @@ Plus per-chunk counts and quarter offsets and a 96-byte device header (``fc_pack
 """
 from __future__ import annotations
 
-import contextlib
 import ctypes
 import threading
 import weakref
@@ -177,16 +176,50 @@ def encode_top(g: torch.Tensor, k: int, *, key_mode: int = L.FC_KEY_MAGNITUDE, s
         packet = Packet.alloc(n, L.FC_FMT_IDXVAL, g.device, k=k)
     packet.k = k
     fn = lib.fc_topk_encode_exact if exact else lib.fc_topk_encode
-    fused = not exact and key_mode == L.FC_KEY_MAGNITUDE and 0 < k < n
-    with (_fused_encode(g.device) if fused else contextlib.nullcontext()):
-        L.check(fn(_vp(g), n, k, key_mode, seed, offset, _vp(packet.idx), _vp(packet.val),
-                   packet.capacity, _vp(packet.cnt), _vp(packet.qoff), _vp(packet.hdr), _vp(ws.buf),
-                   ws.nbytes, _stream(g.device)), "fc_topk_encode")
+    L.check(fn(_vp(g), n, k, key_mode, seed, offset, _vp(packet.idx), _vp(packet.val),
+               packet.capacity, _vp(packet.cnt), _vp(packet.qoff), _vp(packet.hdr), _vp(ws.buf),
+               ws.nbytes, _stream(g.device)), "fc_topk_encode")
     packet._enc = (g, k, key_mode, seed, offset)
     packet._dense_only = False
     if check:
         resolve([packet])
     return packet
+
+
+def encode_decode_top(g: torch.Tensor, k: int, *, packet: Optional[Packet] = None,
+                      out: Optional[torch.Tensor] = None, check: bool = True):
+    """compression.py:31-37 as a packet AND its dense decode (fc_topk_encode_decode): the
+    packet fc_topk_encode writes (entries, counts, quarter offsets, header with T64), and
+    ``out`` = decode(packet), with the resolve's gather and finish done by the decode launch
+    itself (k_fused_mag -> k_beta -> k_decode_res; no gather launch in between).  Returns
+    (packet, out).  ``check=False`` skips the status read (call :func:`resolve` and, if it
+    re-encoded, :func:`decode` yourself)."""
+    _require_cuda_f32(g)
+    n = g.numel()
+    if not 0 <= k <= n:
+        raise ValueError(f"k={k} outside [0, {n}]")
+    if out is None:
+        out = torch.empty(n, dtype=torch.float32, device=g.device)
+    _require_cuda_f32(out, "out")
+    if out.numel() != n:
+        raise ValueError("out must have n elements")
+    if packet is None:
+        packet = Packet.alloc(n, L.FC_FMT_IDXVAL, g.device, k=k)
+    if k == 0 or k >= n:                       # trivial thresholds: the exact engine's packet
+        encode_top(g, k, packet=packet, check=check)
+        return packet, decode(packet, out=out)
+    lib = L.load()
+    ws = Workspace.get(n, g.device)
+    packet.k = k
+    L.check(lib.fc_topk_encode_decode(_vp(g), n, k, _vp(packet.idx), _vp(packet.val),
+                                      packet.capacity, _vp(packet.cnt), _vp(packet.qoff),
+                                      _vp(packet.hdr), _vp(ws.buf), ws.nbytes, _vp(out),
+                                      _stream(g.device)), "fc_topk_encode_decode")
+    packet._enc = (g, k, L.FC_KEY_MAGNITUDE, 0, 0)
+    packet._dense_only = False
+    if check and resolve([packet]):            # bracket missed: exact packet, then decode
+        decode(packet, out=out)
+    return packet, out
 
 
 def compress_top_dense(g: torch.Tensor, k: int, out: Optional[torch.Tensor] = None,
@@ -212,11 +245,10 @@ def compress_top_dense(g: torch.Tensor, k: int, out: Optional[torch.Tensor] = No
     lib = L.load()
     ws = Workspace.get(n, g.device)
     packet.k = k
-    with _fused_encode(g.device):
-        L.check(lib.fc_topk_encode_dense(_vp(g), n, k, _vp(packet.idx), _vp(packet.val),
-                                         packet.capacity, _vp(packet.cnt), _vp(packet.qoff),
-                                         _vp(packet.hdr), _vp(ws.buf), ws.nbytes, _vp(out),
-                                         _stream(g.device)), "fc_topk_encode_dense")
+    L.check(lib.fc_topk_encode_dense(_vp(g), n, k, _vp(packet.idx), _vp(packet.val),
+                                     packet.capacity, _vp(packet.cnt), _vp(packet.qoff),
+                                     _vp(packet.hdr), _vp(ws.buf), ws.nbytes, _vp(out),
+                                     _stream(g.device)), "fc_topk_encode_dense")
     packet._enc = (g, k, L.FC_KEY_MAGNITUDE, 0, 0)
     packet._dense_only = True
     if check and resolve([packet]):            # bracket missed: exact packet, then decode
@@ -253,40 +285,9 @@ class BatchWorkspace:
 
 _SIDE: dict = {}
 _MAX_SIDE = 4          # GPU_MAX_HW_QUEUES is 4: more forked streams would share queues
-# One kernel holds workgroups in an in-kernel wait: k_fused_mag, the lone magnitude encode
-# (fc_topk_encode, fc_topk_encode_dense), whose compaction workgroups poll for the bracket its
-# sample workgroups publish.  Two such launches on two queues are dispatched to the 8 XCDs
-# interleaved, so an XCD can fill up with waiters whose partners are queued on another full
-# XCD (round 4 measured this stall, to the spin bound, with the then-waiting k_resolve).  Every
-# fused encode on a device is therefore queued after the device's previous one when that one
-# went to another stream: the device remembers the stream of its last fused encode, and a
-# fused encode on ANOTHER stream records an event on that stream at that moment and waits for
-# it (everything queued there so far, the previous fused encode included).  Calls on one stream
-# record nothing: an event recorded after every fused encode cost ~3 us per call at 16 M
-# (dense 47.9 -> 44.2-45.0 us, the HIP-graph figure; profiles/r05_ab_order_events.jsonl).
-# Every other encode kernel — batched, mask, rand-k, fp64, exact — has only last-arriver
-# tickets and runs beside anything.
-_FUSED_LAST: dict = {}                  # device index -> stream of its last fused encode
-_FUSED_LOCK = threading.RLock()
-
-
-@contextlib.contextmanager
-def _fused_encode(dev: torch.device):
-    """Queue the fused encode launched inside this block after the device's previous fused
-    encode (held under a lock, so another host thread cannot slip in between)."""
-    key = dev.index if dev.index is not None else torch.cuda.current_device()
-    stream = torch.cuda.current_stream(dev)
-    if torch.cuda.is_current_stream_capturing():        # GraphedCalls: the graph orders its own
-        yield                                           # calls; no events across the capture
-        return
-    with _FUSED_LOCK:
-        last = _FUSED_LAST.get(key)
-        if last is not None and last != stream:
-            ev = torch.cuda.Event()
-            ev.record(last)
-            stream.wait_event(ev)
-        yield
-        _FUSED_LAST[key] = stream
+# k_fused_mag / k_fused64 (the lone magnitude encodes) hold workgroups in a bounded in-kernel
+# wait; the library orders those launches per device itself (include/fedcodec.h, Concurrency),
+# so any stream may issue them.  A graph replay is bracketed by fc_fused_order_begin / _end.
 
 
 def _side_streams(dev: torch.device, count: int = 2) -> list:
@@ -524,8 +525,14 @@ class GraphedCalls:
         torch.cuda.current_stream(dev).wait_stream(self.stream)
 
     def replay(self) -> None:
-        """Launch the captured calls on the current stream."""
+        """Launch the captured calls on the current stream, ordered after the device's last
+        in-kernel-waiting encode (fc_fused_order_begin / _end: the library's own ordering does
+        not see launches inside a graph)."""
+        lib = L.load()
+        s = _stream(self.stream.device)
+        L.check(lib.fc_fused_order_begin(s), "fc_fused_order_begin")
         self.graph.replay()
+        L.check(lib.fc_fused_order_end(s), "fc_fused_order_end")
 
 
 def resolve(packets: Sequence[Packet]) -> int:

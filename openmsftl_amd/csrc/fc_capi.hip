@@ -7,6 +7,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <mutex>
 #include <vector>
 
 // Part of the unity build (fedcodec.hip): the kernels and their argument structs from
@@ -51,6 +52,7 @@ static WsPtrs ws_ptrs(void* ws, uint64_t n) {
   W.ehist = reinterpret_cast<uint32_t*>(b + L.off_ehist);
   W.chist = reinterpret_cast<uint32_t*>(b + L.off_chist);
   W.small = reinterpret_cast<uint64_t*>(b + L.off_small);
+  W.smallv = reinterpret_cast<uint32_t*>(b + L.off_smallv);
   W.pub = reinterpret_cast<uint32_t*>(b + L.off_pub);
   W.ccnt = reinterpret_cast<uint32_t*>(b + L.off_status);
   W.cand = reinterpret_cast<uint64_t*>(b + L.off_cand);
@@ -309,8 +311,98 @@ static bool fused_enabled() {
 #endif
 }
 
+// ---- per-device ordering of the launches whose workgroups wait in-kernel -------------------
+// k_fused_mag and k_fused64 hold their compaction workgroups in a bounded poll for the bracket
+// their own sample workgroups publish.  Two such launches on two streams are dispatched to the
+// XCDs interleaved, so an XCD can fill with waiters whose partners are queued behind another
+// full XCD (a stall to the poll bound, then RETRY).  The library itself queues every such launch
+// of a device after the previous one: it records its event on the launch's stream after each
+// launch and, when the next one comes on another stream, makes that stream wait for the event.
+// A stream being captured into a graph is left alone (a replay is ordered by
+// fc_fused_order_begin / _end around it).
+namespace {
+struct FusedOrder {
+  std::mutex mu;
+  hipEvent_t ev = nullptr;
+  hipStream_t last = nullptr;
+  bool pending = false;
+};
+constexpr int kMaxDevices = 64;
+FusedOrder g_fused_order[kMaxDevices];
+
+int stream_device(hipStream_t s) {
+  int dev = 0;
+  if (s == nullptr || hipStreamGetDevice(s, &dev) != hipSuccess) (void)hipGetDevice(&dev);
+  return dev & (kMaxDevices - 1);
+}
+
+bool capturing(hipStream_t s) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+}
+
+class FusedGuard {
+ public:
+  explicit FusedGuard(hipStream_t s) : s_(s) {
+    if (capturing(s)) return;
+    const int dev = stream_device(s);
+    F_ = &g_fused_order[dev];
+    F_->mu.lock();
+    if (!F_->ev) {
+      int cur = 0;
+      (void)hipGetDevice(&cur);
+      if (cur != dev) (void)hipSetDevice(dev);
+      (void)hipEventCreateWithFlags(&F_->ev, hipEventDisableTiming);
+      if (cur != dev) (void)hipSetDevice(cur);
+    }
+    if (F_->pending && F_->last != s) (void)hipStreamWaitEvent(s, F_->ev, 0);
+  }
+  ~FusedGuard() {
+    if (!F_) return;
+    (void)hipEventRecord(F_->ev, s_);
+    F_->last = s_;
+    F_->pending = true;
+    F_->mu.unlock();
+  }
+  FusedGuard(const FusedGuard&) = delete;
+  FusedGuard& operator=(const FusedGuard&) = delete;
+
+ private:
+  hipStream_t s_;
+  FusedOrder* F_ = nullptr;
+};
+}  // namespace
+
+extern "C" int fc_fused_order_begin(fc_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  FusedOrder& F = g_fused_order[stream_device(s)];
+  std::lock_guard<std::mutex> g(F.mu);
+  if (F.pending && F.last != s && hipStreamWaitEvent(s, F.ev, 0) != hipSuccess)
+    return fail(FC_ERR_HIP, "fc_fused_order_begin: hipStreamWaitEvent");
+  return FC_OK;
+}
+
+extern "C" int fc_fused_order_end(fc_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int dev = stream_device(s);
+  FusedOrder& F = g_fused_order[dev];
+  std::lock_guard<std::mutex> g(F.mu);
+  if (!F.ev) {
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    if (cur != dev) (void)hipSetDevice(dev);
+    (void)hipEventCreateWithFlags(&F.ev, hipEventDisableTiming);
+    if (cur != dev) (void)hipSetDevice(cur);
+  }
+  if (hipEventRecord(F.ev, s) != hipSuccess) return fail(FC_ERR_HIP, "fc_fused_order_end: hipEventRecord");
+  F.last = s;
+  F.pending = true;
+  return FC_OK;
+}
+
 static int launch_fused(const CompactArgs& ca, const SamplePlan& P, const HdrInit& hi,
                          uint32_t nsamp, hipStream_t s) {
+  FusedGuard order(s);
   TimedLaunch t(FC_TIME_COMPACT, s);
   const dim3 grid(nsamp + ca.nchunks);
   if (ca.dense) hipLaunchKernelGGL(k_fused_mag<true>, grid, dim3(kCBlock), 0, s, ca, P, hi, nsamp);
@@ -474,6 +566,40 @@ int fc_topk_encode(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_
   if (rc) return rc;
   ra.rbin = 1;                       // the unfused compactions leave the binning to k_resolve
   return launch_resolve(ra, s);
+}
+
+int fc_topk_encode_decode(const float* g, uint64_t n, uint64_t k, uint16_t* idx, float* val,
+                          uint64_t capacity, uint32_t* cnt, uint64_t* qoff, fc_packet_hdr* hdr,
+                          void* ws, size_t ws_bytes, float* out, fc_stream_t stream) {
+  FC_CHECK(k > 0 && k < n, "fc_topk_encode_decode needs 0 < k < n (k=%llu, n=%llu)",
+           (unsigned long long)k, (unsigned long long)n);
+  FC_CHECK(qoff != nullptr, "fc_topk_encode_decode needs the quarter offsets (qoff)");
+  FC_CHECK(out != nullptr && ((uintptr_t)out & 15) == 0, "out must be non-NULL and 16-byte aligned");
+  CompactArgs ca; EngineArgs ea; ResolveArgs ra; HdrInit hi;
+  int rc = topk_args(g, n, k, FC_KEY_MAGNITUDE, 0, 0, idx, val, capacity, cnt, qoff, hdr, ws,
+                     ws_bytes, &ca, &ea, &ra, &hi);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  const SamplePlan P = make_plan(n, k);
+  const uint32_t sgrid = (P.nseg + P.segs - 1) / P.segs;
+  // the packet, exactly fc_topk_encode's; then the bin beta in one workgroup (as the fused
+  // launch's own tail — a last-arriver ticket in every chunk workgroup — it cost more than this
+  // launch: 128 M 141.4 -> 147.1 us, 16 M 35.5 -> 43.5 us, profiles/r06_lone_probe.jsonl)
+  rc = launch_fused(ca, P, hi, sgrid, s);
+  if (rc) return rc;
+  {
+    TimedLaunch t(FC_TIME_ENGINE, s);
+    hipLaunchKernelGGL(k_beta, dim3(1), dim3(kBlock), 0, s, ra);
+    FC_LAUNCHED("k_beta");
+  }
+  DecResArgs d;
+  memset(&d, 0, sizeof d);
+  d.idx = idx; d.val = val; d.qoff = qoff; d.hdr = hdr; d.out = out; d.n = n;
+  d.ib = index_bits(n); d.W = ws_ptrs(ws, n);
+  TimedLaunch t(FC_TIME_DECODE, s);
+  hipLaunchKernelGGL(k_decode_res, dim3(num_chunks(n)), dim3(kQBlock), 0, s, d);
+  FC_LAUNCHED("k_decode_res");
+  return FC_OK;
 }
 
 int fc_topk_encode_dense(const float* g, uint64_t n, uint64_t k, uint16_t* idx, float* val,
@@ -877,6 +1003,7 @@ int fc_topk_dense_f64_sampled(const double* g, uint64_t n, uint64_t k, double* o
   {
     TimedLaunch t(FC_TIME_COMPACT, s);
     const uint32_t nsamp = (P.nseg + P.segs - 1) / P.segs;
+    FusedGuard order(s);
     hipLaunchKernelGGL(k_fused64, dim3(nsamp + a.nchunks), dim3(kBlock), 0, s, a, P, W, ib, hdr, hi, nsamp);
     FC_LAUNCHED("k_fused64");
   }

@@ -31,7 +31,8 @@ struct alignas(16) TopkState {
                          // a launch tags its bracket records (fz_seq + 1) | bit 31
   uint32_t hgen;         // k_resolve: bumped once the bin beta below is published
   uint32_t rb_beta, rb_rin, rb_cnt;   // k_resolve: bin holding rank r, rank inside it, its count
-  uint32_t pad_[3];
+  uint32_t rb_flags;     // k_beta: bit 0 retry (exact path), bit 1 rank 0 (every candidate slack)
+  uint32_t rb_nent, rb_ncand;         // k_beta: entries listed, candidates among them
   uint32_t shard_ent[kShards];   // k_compact totals, 64-way sharded (no hot word)
   uint32_t shard_cnd[kShards];
 };
@@ -62,7 +63,8 @@ constexpr int kPubWords = (kPubCopies + kWinCopies) * kPubStride;
 
 struct WsLayout {
   uint64_t nchunks, cand_cap;
-  uint64_t off_hist1, off_tick, off_ehist, off_chist, off_small, off_pub, off_status, off_cand, bytes;
+  uint64_t off_hist1, off_tick, off_ehist, off_chist, off_small, off_smallv, off_pub, off_status,
+      off_cand, bytes;
   __host__ __device__ static WsLayout of(uint64_t n) {
     WsLayout L;
     L.nchunks = (n + kChunk - 1) / kChunk;
@@ -79,6 +81,7 @@ struct WsLayout {
     o += 8192;
     L.off_chist = o;  o += 4ull * kHistBins * kCandShards;
     L.off_small = o;  o += 8ull * kSmallCap;
+    L.off_smallv = o; o += 4ull * kSmallCap;        // k_decode_res: the gathered entries' values
     L.off_pub = o;    o += 4ull * kPubWords;        // n-independent, like every counter above
     L.off_status = o; o += 4ull * (L.nchunks ? L.nchunks : 1);   // per-chunk candidate counts
     o = (o + 15) & ~15ull;
@@ -98,6 +101,7 @@ struct WsPtrs {
   TopkState* st;
   uint32_t *hist1, *tick, *ehist, *chist;   // hist1: kSampleShards x 4096; tick: 3 tickets
   uint64_t* small;
+  uint32_t* smallv;        // k_decode_res: value bits of small[i]
   uint32_t* pub;           // k_fused_mag publications (kPubWords)
   uint32_t* ccnt;          // candidates per chunk (may exceed kCandSlot: overflowed chunk)
   uint64_t* cand;          // chunk c's candidates at [c * kCandSlot, + min(ccnt, kCandSlot))
@@ -112,6 +116,7 @@ __device__ __forceinline__ WsPtrs ws_shift(WsPtrs W, uint64_t bytes) {
   W.ehist = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(W.ehist) + bytes);
   W.chist = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(W.chist) + bytes);
   W.small = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(W.small) + bytes);
+  W.smallv = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(W.smallv) + bytes);
   W.pub = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(W.pub) + bytes);
   W.ccnt = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(W.ccnt) + bytes);
   W.cand = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(W.cand) + bytes);

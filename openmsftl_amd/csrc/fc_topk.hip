@@ -1092,6 +1092,46 @@ __global__ __launch_bounds__(kCBlock, FC_MAG1_WAVES_PER_EU) void k_compact_mag1_
 // never waits on a chunk workgroup, so no wait can deadlock; a timed-out one (never expected)
 // sets S->err, and the resolve reports RETRY (the caller re-encodes exactly).
 // --------------------------------------------------------------------------------------
+// The resolve's bin search (k_resolve<false>'s head) as one workgroup's work (256 threads): from
+// the shard totals and the candidate histogram of a fused encode, the bin beta holding rank r =
+// k - #(key > t_hi), the rank inside it and its count -> S->rb_*; rb_flags bit 0 = retry (the
+// exact path), bit 1 = rank 0 (T64 = (t_hi + 1) << ib: every candidate is slack).  AGENT: the
+// counters were written in this launch (coherent loads), else by an earlier one.
+template <bool AGENT = false>
+__device__ __forceinline__ void beta_body(const WsPtrs& W, uint64_t k, uint32_t* h, uint32_t* s_tmp,
+                                          uint32_t* s_out, uint32_t* s_tot) {
+  TopkState* S = W.st;
+  const int tid = threadIdx.x;
+  auto ld = [](const uint32_t* p) { return AGENT ? ld_agent(p) : *p; };
+  uint32_t se = 0, sc = 0;
+  if (tid < kShards) { se = ld(&S->shard_ent[tid]); sc = ld(&S->shard_cnd[tid]); }
+  const uint32_t err = ld(&S->err);
+#pragma unroll
+  for (int j = 0; j < kHistBins / kBlock; ++j) h[j * kBlock + tid] = ld(&W.chist[j * kBlock + tid]);
+  if (tid < 64) {
+    se = wave_sum(se);
+    sc = wave_sum(sc);
+    if (tid == 0) { s_tot[0] = se; s_tot[1] = sc; }
+  }
+  __syncthreads();
+  const uint32_t n_ent = s_tot[0], n_cand = s_tot[1];
+  const uint32_t n_hi = n_ent - n_cand;
+  const bool bad = err || n_cand > n_ent || (uint64_t)n_ent < k || (uint64_t)n_hi > k;
+  const uint32_t rank = bad ? 0u : (uint32_t)(k - n_hi);
+  bool retry = bad;
+  uint32_t beta = 0xffffffffu, r_in = 1, cnt = 0;
+  if (!retry && rank > 0) {
+    find_rank_desc(h, rank, s_tmp, s_out);
+    beta = s_out[0]; r_in = s_out[1]; cnt = h[beta];
+    retry = cnt > (uint32_t)kSmallCap || cnt < r_in;
+  }
+  if (tid == 0) {
+    S->rb_beta = beta; S->rb_rin = r_in; S->rb_cnt = cnt;
+    S->rb_flags = (retry ? 1u : 0u) | (!retry && rank == 0 ? 2u : 0u);
+    S->rb_nent = n_ent; S->rb_ncand = n_cand;
+  }
+}
+
 union FusedShared {
   SampleShared s;
   MagShared m;
@@ -1459,6 +1499,19 @@ __global__ __launch_bounds__(kBlock) void k_resolve(ResolveArgs a0) {
 }
 template __global__ void k_resolve<true>(ResolveArgs);
 template __global__ void k_resolve<false>(ResolveArgs);
+
+// --------------------------------------------------------------------------------------
+// k_beta: the head of k_resolve<false> alone, for a lone fused packet encode whose gather and
+// finish run inside its decode (fc_topk_encode_decode -> k_decode_res): from the shard totals
+// and the candidate histogram k_fused_mag filled, the bin beta holding rank r = k - #(key >
+// t_hi), the rank inside it and its count -> S->rb_*; rb_flags bit 0 = retry (the exact path),
+// bit 1 = rank 0 (T64 = (t_hi + 1) << ib: every candidate is slack).  One workgroup.
+// --------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_beta(ResolveArgs a) {
+  __shared__ uint32_t h[kHistBins];
+  __shared__ uint32_t s_tmp[8], s_out[4], s_tot[2];
+  beta_body<false>(a.W, a.k, h, s_tmp, s_out, s_tot);
+}
 
 
 // --------------------------------------------------------------------------------------
