@@ -34,8 +34,11 @@ def install(aggregator: bool = True, devices=None):
     """Swap the codec (and by default the aggregator's hot path) into ``ftl``.  Returns the
     patched ``ftl.gradient_aggregation.aggregation`` module (or None with aggregator=False).
     ``devices``: the GPUs the streamed aggregation fans out over when an aggregator's config
-    names none ("all", a count or a list of indices; None = the current device only)."""
-    aggregation.DEFAULT_DEVICES = devices
+    names none ("all", a count or a list of indices).  Left out (None), an earlier setting is
+    kept; the initial default is the current device only (multi-GPU fan-out
+    is opt-in, ``install(devices="all")``)."""
+    if devices is not None:
+        aggregation.DEFAULT_DEVICES = devices
     sys.modules["ftl.compression"] = compression                  # experiment.py:7
     sys.modules["ftl.compression.compression"] = compression      # client.py:8
     for name in ("ftl.agents.client", "ftl.experiment"):          # already imported: re-point
@@ -52,6 +55,7 @@ def install(aggregator: bool = True, devices=None):
         cls._ref_aggregate_grads = cls.aggregate_grads
     cls.aggregate_grads = aggregation.aggregate_grads
     cls.agg_path = None
+    cls.agg_draws = None
     return ref_agg
 
 

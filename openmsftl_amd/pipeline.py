@@ -123,7 +123,14 @@ class RowPlan:
     ``lookahead`` rows ahead of the pipeline, into pinned buffers that the pipeline copies H2D.
     Several pipeline threads (:class:`DeviceRing`) may take masks; the draw order never
     changes.  :meth:`close` waits for the producer (every draw done: the RNG is then where the
-    reference leaves it) and re-raises a draw's exception (e.g. NumPy's ValueError for p > 1)."""
+    reference leaves it) and re-raises a draw's exception (e.g. NumPy's ValueError for p > 1).
+
+    Error path: if the round fails for another reason (a FedCodecError, an H2D or
+    allocation error) and the plan is closed with ``wait=False``, host draws may already have
+    run up to ``lookahead`` rows past the failing row, so np.random is then further along than
+    the reference's loop would have left it; device MT19937 rows ("mt") leave np.random at the
+    round's start instead.  A caller that must resume the stream exactly after such an error
+    saves ``np.random.get_state()`` before the round and restores it."""
 
     def __init__(self, n: int, specs: Sequence[RowCodec], draws: Optional[dict] = None,
                  lookahead: int = 8, base: int = 0, parent: "RowPlan" = None,
