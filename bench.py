@@ -532,57 +532,61 @@ def single_gradient(torch, codec, g, k, n, iters=None, graph=True):
     """North-star probe: encode+decode of ONE 128 M gradient (packet -> dense), HBM fraction
     of the algorithmic 8N + 16k bytes.  Host wall clock over ``iters``
     back-to-back calls: 20 at 128 M, 200 below 64 M elements, so that the first launch's host
-    latency and the final synchronise (~30-50 us once per loop) stay below 1 % of the loop."""
+    latency and the final synchronise (~30-50 us once per loop) stay below 1 % of the loop.
+    The round trip is fc_topk_encode_decode (the packet of fc_topk_encode, then its dense
+    decode, the resolve's gather and finish done inside the decode launch); ``two_calls`` is
+    the same packet and q from fc_topk_encode (+ k_resolve) and fc_decode_dense."""
     if iters is None:
         iters = 20 if n >= (1 << 26) else 200
     out = torch.empty_like(g)
     pkt = codec.encode_top(g, k)
-    for _ in range(3):
-        codec.encode_top(g, k, packet=pkt, check=False)
-        codec.decode(pkt, out=out)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(iters):
-        codec.encode_top(g, k, packet=pkt, check=False)
-        codec.decode(pkt, out=out)
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / iters
-    codec.resolve([pkt])
+
+    def timed(fn):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            fn()
+        torch.cuda.synchronize()
+        dt_ = (time.perf_counter() - t0) / iters
+        codec.resolve([pkt])
+        return dt_
+
+    roundtrip = lambda: codec.encode_decode_top(g, k, packet=pkt, out=out, check=False)   # noqa: E731
+    two_calls = lambda: (codec.encode_top(g, k, packet=pkt, check=False),                 # noqa: E731
+                         codec.decode(pkt, out=out))
+    dense = lambda: codec.compress_top_dense(g, k, out=out, packet=pkt, check=False)     # noqa: E731
+    dt = timed(roundtrip)
+    dt_2 = timed(two_calls)
     # the same result through fc_topk_encode_dense (compaction streams q, fix-up of the slack)
-    for _ in range(3):
-        codec.compress_top_dense(g, k, out=out, packet=pkt, check=False)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(iters):
-        codec.compress_top_dense(g, k, out=out, packet=pkt, check=False)
-    torch.cuda.synchronize()
-    dt_d = (time.perf_counter() - t0) / iters
+    dt_d = timed(dense)
     moved = dense_moved_bytes(n, pkt)
     codec.resolve([pkt])
     alg = 8.0 * n + 2 * ENTRY_BYTES * k
+    frac = lambda t: round(alg / t / 1e9 / HBM_PEAK_GBPS, 4)                               # noqa: E731
     res = {"n": n, "k": k, "us_per_encode_decode": round(dt * 1e6, 1),
            "grad_GBps": round(4.0 * n / dt / 1e9, 1),
            "alg_GBps": round(alg / dt / 1e9, 1),
-           "hbm_frac": round(alg / dt / 1e9 / HBM_PEAK_GBPS, 4),
+           "hbm_frac": frac(dt),
+           "path": "fc_topk_encode_decode (k_fused_mag<false> -> k_beta -> k_decode_res)",
+           "two_calls": {"us": round(dt_2 * 1e6, 1), "hbm_frac": frac(dt_2),
+                         "path": "fc_topk_encode (k_fused_mag<false> -> k_resolve) + fc_decode_dense"},
            "fused_dense": {"us": round(dt_d * 1e6, 1),
                            "alg_GBps": round(alg / dt_d / 1e9, 1),
-                           "hbm_frac": round(alg / dt_d / 1e9 / HBM_PEAK_GBPS, 4),
+                           "hbm_frac": frac(dt_d),
                            "moved_bytes": int(moved),
                            "hbm_frac_moved": round(moved / dt_d / 1e9 / HBM_PEAK_GBPS, 4)}}
     if not graph:                      # (N > 1: no graph capture beside a live process group)
         return res
     # the same calls, `iters` of them captured in one HIP graph (codec.GraphedCalls) and
     # replayed: no host work per call, cheaper kernel boundaries; same kernels, same buffers
-    dt_g = _graph_us(torch, codec, lambda: (codec.encode_top(g, k, packet=pkt, check=False),
-                                            codec.decode(pkt, out=out)), iters) * 1e-6
+    dt_g = _graph_us(torch, codec, roundtrip, iters) * 1e-6
     codec.resolve([pkt])
-    dt_dg = _graph_us(torch, codec, lambda: codec.compress_top_dense(g, k, out=out, packet=pkt,
-                                                                     check=False), iters) * 1e-6
+    dt_dg = _graph_us(torch, codec, dense, iters) * 1e-6
     codec.resolve([pkt])
-    res["graph"] = {"us_per_encode_decode": round(dt_g * 1e6, 1),
-                    "hbm_frac": round(alg / dt_g / 1e9 / HBM_PEAK_GBPS, 4)}
-    res["fused_dense"]["graph"] = {"us": round(dt_dg * 1e6, 1),
-                                   "hbm_frac": round(alg / dt_dg / 1e9 / HBM_PEAK_GBPS, 4),
+    res["graph"] = {"us_per_encode_decode": round(dt_g * 1e6, 1), "hbm_frac": frac(dt_g)}
+    res["fused_dense"]["graph"] = {"us": round(dt_dg * 1e6, 1), "hbm_frac": frac(dt_dg),
                                    "hbm_frac_moved": round(moved / dt_dg / 1e9 / HBM_PEAK_GBPS, 4)}
     return res
 
@@ -680,13 +684,13 @@ def codec_matrix(torch, codec, L, device, n16=16_777_216, n25=25_557_032):
         out = out16 if n == n16 else torch.empty_like(g)
         k = kept_count(0.01, n)
         pkt = codec.encode_top(g, k)
-        us = _time_us(torch, lambda: (codec.encode_top(g, k, packet=pkt, check=False),
-                                      codec.decode(pkt, out=out)))
+        us = _time_us(torch, lambda: codec.encode_decode_top(g, k, packet=pkt, out=out, check=False))
+        assert codec.resolve([pkt]) == 0
         usd = _time_us(torch, lambda: codec.compress_top_dense(g, k, out=out, packet=pkt, check=False))
         moved = dense_moved_bytes(n, pkt)
         assert codec.resolve([pkt]) == 0
         alg = 8.0 * n + 16.0 * k
-        rows[name] = _row(us, alg, n=n, k=k, path="fc_topk_encode + fc_decode_dense",
+        rows[name] = _row(us, alg, n=n, k=k, path="fc_topk_encode_decode (packet + dense decode)",
                           dense=_row(usd, alg, path="fc_topk_encode_dense", moved_bytes=int(moved),
                                      hbm_frac_moved=round(moved / usd / 1e3 / HBM_PEAK_GBPS, 4)))
     # rand f = 0.1 at 16 M: native Philox keys (fc_topk_encode PHILOX) and parity mode (the

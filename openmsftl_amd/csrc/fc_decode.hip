@@ -910,15 +910,15 @@ __global__ __launch_bounds__(kQBlock, 4) void k_fold_q(DecodeArgs a) {
 // --------------------------------------------------------------------------------------
 // k_decode_res: the dense decode of a lone fused packet encode that also finishes its resolve
 // (fc_topk_encode_decode), so no gather launch sits between encode and decode.  k_beta has
-// placed the bin beta of the candidate histogram that holds rank r; every entry the packet lists
-// is, by its key, definite (above the bracket: kept), a candidate binned above beta (kept),
-// below beta (slack: below T64 whatever T64 is) or in bin beta.  The quarter-owned waves of
-// k_fold_q<false, true> assign the kept entries into their tile; a bin-beta entry goes to the
-// small list (comp + value bits) and its location is NOT written by this workgroup.  The last
-// arriver (two-level ticket) ranks the <= 4096 bin-beta entries, writes T64 and the header
-// exactly as k_resolve's last arriver does, and stores each bin-beta location once: its value if
-// comp >= T64, else +0.  Every output byte thus has one writer in the launch (no cross-XCD
-// ordering of two stores to one address is needed).
+// placed the bin beta of the candidate histogram that holds rank r (and closed the header and the
+// state when bin beta needs no ranking); every entry the packet lists is, by its key, definite
+// (above the bracket: kept), a candidate binned above beta (kept), below beta (slack: below T64
+// whatever T64 is) or in bin beta.  The quarter-owned waves of k_fold_q<false, true> assign the
+// kept entries into their tile; a bin-beta entry goes to the small list (comp + value bits) and
+// its location is NOT written by this workgroup.  The workgroup that stores bin beta's last entry
+// (k_beta counted them: a counter, not a ticket in every workgroup) ranks the list, writes T64
+// and stores each bin-beta location once: its value if comp >= T64, else +0.  Every output byte
+// thus has one writer in the launch.
 // --------------------------------------------------------------------------------------
 struct DecResArgs {
   const uint16_t* idx;
@@ -932,9 +932,9 @@ struct DecResArgs {
 };
 
 __global__ __launch_bounds__(kQBlock, 4) void k_decode_res(DecResArgs a) {
-  __shared__ __attribute__((aligned(16))) float tile[kChunk];    // the last arriver: its sort list
+  __shared__ __attribute__((aligned(16))) float tile[kChunk];    // the finisher: its sort list
   __shared__ uint32_t s_skip[4][kQuarter / 32];                 // bin-beta locations per quarter
-  __shared__ uint32_t s_flag;
+  __shared__ uint32_t s_last;
   __shared__ uint64_t s_T;
   const int tid = threadIdx.x, lane = lane_id();
   const int q = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -943,16 +943,17 @@ __global__ __launch_bounds__(kQBlock, 4) void k_decode_res(DecResArgs a) {
   const uint32_t qbase = (uint32_t)base + (uint32_t)(q * kQuarter);
   TopkState* S = a.W.st;
   const uint32_t t_lo = S->t_lo, t_hi = S->t_hi, sbin = S->sbin;
-  const uint32_t beta = S->rb_beta, flags = S->rb_flags;
-  const bool retry = (flags & 1u) != 0;
+  const uint32_t beta = S->rb_beta, flags = S->rb_flags, cnt = S->rb_cnt;
+  const bool gather = (flags & 3u) == 0;                         // not retry, not rank 0
   float* qt = tile + q * kQuarter;
 #pragma unroll
   for (int i = 0; i < kQuarter / 256; ++i)
     *reinterpret_cast<float4*>(&qt[i * 256 + lane * 4]) = make_float4(0.f, 0.f, 0.f, 0.f);
   s_skip[q][lane] = 0u;
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  if (!retry) {
+  if (tid == 0) s_last = 0u;
+  __syncthreads();
+  bool finisher = false;
+  if (!(flags & 1u)) {
     const uint64_t qo = a.qoff[c];
     const uint32_t st = q == 0 ? 0u : (uint32_t)(qo >> (16 * (q - 1))) & 0xffffu;
     const uint32_t en = q == 3 ? (uint32_t)(qo >> 48) : (uint32_t)(qo >> (16 * q)) & 0xffffu;
@@ -967,16 +968,17 @@ __global__ __launch_bounds__(kQBlock, 4) void k_decode_res(DecResArgs a) {
       const bool cand = key <= t_hi;
       if (!cand || bin > beta) {                                 // beta = ~0 (rank 0): none
         qt[loc] = v;
-      } else if (bin == beta) {
-        const uint32_t pos = atomicAdd(&S->small_n, 1u);
-        if (pos < (uint32_t)kSmallCap) {
-          st_agent(&a.W.small[pos], comp_of(key, (uint32_t)base + lc, a.ib));
-          st_agent(&a.W.smallv[pos], __float_as_uint(v));
-        }
+      } else if (bin == beta && gather) {
+        const uint32_t pos = atomicAdd(&S->small_n, 1u);        // < cnt <= kSmallCap (k_beta)
+        st_agent(&a.W.small[pos], comp_of(key, (uint32_t)base + lc, a.ib));
+        st_agent(&a.W.smallv[pos], __float_as_uint(v));
         atomicOr(&s_skip[q][loc >> 5], 1u << (loc & 31));
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");        // the entry is stored ...
+        if (atomicAdd(&S->small_done, 1u) == cnt - 1u) finisher = true;   // ... then counted
       }
     }
   }
+  if (finisher) s_last = 1u;
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   __builtin_amdgcn_wave_barrier();
   float* out = a.out;
@@ -995,55 +997,42 @@ __global__ __launch_bounds__(kQBlock, 4) void k_decode_res(DecResArgs a) {
       if (!(skip & 8u) && e + 3 < a.n) out[e + 3] = v.w;
     }
   }
-  if (!last_block_arrive_tree(a.W.tick + kTickWords, gridDim.x, blockIdx.x, &s_flag, 16)) return;
-  // ---- last workgroup: T64 = the r_in-th largest of bin beta, its locations, the header ----
+  if (!gather) return;                                           // uniform
+  __syncthreads();
+  if (!s_last) return;
+  // ---- the finisher: T64 = the r_in-th largest of bin beta, its locations, the header ----
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   uint64_t* sv = reinterpret_cast<uint64_t*>(tile);               // 4096 comps
-  const uint32_t n_ent = S->rb_nent, n_cand = S->rb_ncand, r_in = S->rb_rin, cnt = S->rb_cnt;
-  const uint32_t got = min(ld_agent(&S->small_n), (uint32_t)kSmallCap);
-  bool bad = retry;
-  uint64_t T = 0;
-  if (!bad && (flags & 2u)) {
-    T = ((uint64_t)t_hi + 1) << a.ib;                            // exactly the definite set
-  } else if (!bad) {
-    bad = got != cnt || got < r_in;
-    if (!bad && got <= (uint32_t)kQBlock) {
-      uint64_t mine = 0;
-      if ((uint32_t)tid < got) { mine = ld_agent(&a.W.small[tid]); sv[tid] = mine; }
-      __syncthreads();
-      if ((uint32_t)tid < got) {
-        uint32_t larger = 0;
-        for (uint32_t j = 0; j < got; ++j) larger += sv[j] > mine ? 1u : 0u;
-        if (larger == r_in - 1) s_T = mine;
-      }
-      __syncthreads();
-      T = s_T;
-    } else if (!bad) {
-      uint32_t P2 = 1;
-      while (P2 < got) P2 <<= 1;
-      for (uint32_t i = tid; i < P2; i += kQBlock) sv[i] = i < got ? ld_agent(&a.W.small[i]) : 0ull;
-      __syncthreads();
-      bitonic_desc(sv, P2);
-      T = sv[r_in - 1];
+  const uint32_t r_in = S->rb_rin;
+  uint64_t T;
+  if (cnt <= (uint32_t)kQBlock) {
+    uint64_t mine = 0;
+    if ((uint32_t)tid < cnt) { mine = ld_agent(&a.W.small[tid]); sv[tid] = mine; }
+    __syncthreads();
+    if ((uint32_t)tid < cnt) {
+      uint32_t larger = 0;
+      for (uint32_t j = 0; j < cnt; ++j) larger += sv[j] > mine ? 1u : 0u;
+      if (larger == r_in - 1) s_T = mine;
     }
+    __syncthreads();
+    T = s_T;
+  } else {
+    uint32_t P2 = 1;
+    while (P2 < cnt) P2 <<= 1;
+    for (uint32_t i = tid; i < P2; i += kQBlock) sv[i] = i < cnt ? ld_agent(&a.W.small[i]) : 0ull;
+    __syncthreads();
+    bitonic_desc(sv, P2);
+    T = sv[r_in - 1];
   }
-  const bool other_err = ld_agent(&S->err) != 0u;
-  const uint32_t status = bad || other_err ? (uint32_t)FC_STATUS_RETRY_EXACT : (uint32_t)FC_STATUS_OK;
   const uint64_t imask = (1ull << a.ib) - 1;
-  if (status == FC_STATUS_OK)
-    for (uint32_t i = tid; i < got; i += kQBlock) {
-      const uint64_t comp = ld_agent(&a.W.small[i]);
-      const uint32_t vb = ld_agent(&a.W.smallv[i]);
-      out[comp & imask] = comp >= T ? __uint_as_float(vb) : 0.0f;
-    }
-  for (int b = tid; b < kHistBins; b += kQBlock) a.W.chist[b] = 0;   // the compaction's bins
+  for (uint32_t i = tid; i < cnt; i += kQBlock) {
+    const uint64_t comp = ld_agent(&a.W.small[i]);
+    const uint32_t vb = ld_agent(&a.W.smallv[i]);
+    out[comp & imask] = comp >= T ? __uint_as_float(vb) : 0.0f;
+  }
   if (tid == 0) {
     a.hdr->thresh = T;
-    a.hdr->n_entries = n_ent;
-    if (status != FC_STATUS_OK) a.hdr->status = status;
-    a.hdr->n_definite = n_ent - n_cand;
-    a.hdr->n_cand = n_cand;
-    S->small_n = 0; S->err = 0;
-    S->fz_seq += 1u;               // k_fused_mag: the next launch publishes fz_seq + 1
+    S->small_n = 0; S->small_done = 0;
   }
 }
 

@@ -26,7 +26,7 @@ struct alignas(16) TopkState {
   uint32_t small_n;      // survivors gathered for the LDS finish
   uint32_t e_shift, e_rank, e_matched, e_done, e_ticket, e_status;
   uint32_t gen;          // k_resolve generation: bumped when T64 is published (dense fix-up)
-  uint32_t fz_pub;       // (unused: k_fused_mag's bracket records live in WsPtrs::pub)
+  uint32_t small_done;   // k_decode_res: bin-beta entries stored (the last one finishes T64)
   uint32_t fz_seq;       // k_fused_mag launches completed (bumped by the following k_resolve);
                          // a launch tags its bracket records (fz_seq + 1) | bit 31
   uint32_t hgen;         // k_resolve: bumped once the bin beta below is published

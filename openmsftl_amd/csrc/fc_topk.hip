@@ -1507,10 +1507,28 @@ template __global__ void k_resolve<false>(ResolveArgs);
 // t_hi), the rank inside it and its count -> S->rb_*; rb_flags bit 0 = retry (the exact path),
 // bit 1 = rank 0 (T64 = (t_hi + 1) << ib: every candidate is slack).  One workgroup.
 // --------------------------------------------------------------------------------------
+// k_beta also closes what needs no decode: the header's counts, T64 and the status when no entry
+// of bin beta is left to rank (rank 0: T64 = (t_hi + 1) << ib; retry: RETRY), and the state the
+// fused launch leaves (candidate histogram cleared, err reset, fz_seq bumped) — so the decode's
+// workgroups take no last-arriver ticket: the one that stores bin beta's last entry finishes T64.
 __global__ __launch_bounds__(kBlock) void k_beta(ResolveArgs a) {
   __shared__ uint32_t h[kHistBins];
   __shared__ uint32_t s_tmp[8], s_out[4], s_tot[2];
   beta_body<false>(a.W, a.k, h, s_tmp, s_out, s_tot);
+  TopkState* S = a.W.st;
+  const int tid = threadIdx.x;
+  for (int b = tid; b < kHistBins; b += kBlock) a.W.chist[b] = 0;    // read by beta_body (barrier)
+  if (tid == 0) {
+    const uint32_t flags = S->rb_flags, n_ent = S->rb_nent, n_cand = S->rb_ncand;
+    a.hdr->n_entries = n_ent;
+    a.hdr->n_definite = n_ent - n_cand;
+    a.hdr->n_cand = n_cand;
+    if (flags & 1u) { a.hdr->thresh = 0; a.hdr->status = FC_STATUS_RETRY_EXACT; }
+    else if (flags & 2u) a.hdr->thresh = ((uint64_t)S->t_hi + 1) << a.ib;
+    S->err = 0;
+    S->small_n = 0; S->small_done = 0;
+    S->fz_seq += 1u;               // k_fused_mag: the next launch publishes fz_seq + 1
+  }
 }
 
 
