@@ -64,7 +64,7 @@ def parse():
                          "encoded (codec.encode_fold_batch; measured no faster, A/B only)")
     ap.add_argument("--no-batch", action="store_true",
                     help="encode client by client (fc_topk_encode) instead of batched")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r05_pmc_k_compact_mag1.json"),
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r06_pmc_k_compact_mag1.json"),
                     help="PMC summary (profiles/) used for roofline.traffic")
     ap.add_argument("--force-retry-rank", type=int, default=-1,
                     help="test only: on this rank, mark client 0's packet RETRY in the last "
