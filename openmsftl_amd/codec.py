@@ -102,6 +102,26 @@ class Packet:
                    qoff=torch.empty(nch, dtype=torch.int64, device=device)
                    if fmt == L.FC_FMT_IDXVAL else None)
 
+    @classmethod
+    def alloc_batch(cls, n: int, m: int, fmt: int, device, k: int = 0) -> list:
+        """``m`` packets of length n whose fields are the rows of per-field slabs (one (m, cap)
+        value tensor, one index tensor, ...): the layout a batch of G's rows would have.  The
+        128-client 16 M batched compaction writes them 2-3 % faster than m separate allocations
+        (profiles/r05_stagger_probe.jsonl); the packets are ordinary Packet objects."""
+        lib = L.load()
+        nch = int(lib.fc_num_chunks(n))
+        cap = int(lib.fc_packet_capacity(n))
+        val = torch.empty((m, cap), dtype=torch.float32, device=device)
+        idx = torch.empty((m, cap), dtype=_U16, device=device) if fmt == L.FC_FMT_IDXVAL else None
+        bitmap = torch.empty((m, nch * 256), dtype=_U32, device=device) if fmt == L.FC_FMT_BITMAP else None
+        cnt = torch.empty((m, nch), dtype=_U32, device=device)
+        qoff = torch.empty((m, nch), dtype=torch.int64, device=device) if fmt == L.FC_FMT_IDXVAL else None
+        hdr = torch.empty((m, L.HDR_BYTES), dtype=torch.uint8, device=device)
+        return [cls(n=n, fmt=fmt, k=k, val=val[i], cnt=cnt[i], hdr=hdr[i],
+                    idx=idx[i] if idx is not None else None,
+                    bitmap=bitmap[i] if bitmap is not None else None,
+                    qoff=qoff[i] if qoff is not None else None) for i in range(m)]
+
     @property
     def capacity(self) -> int:
         return self.val.numel()
