@@ -622,8 +622,9 @@ def small_configs(torch, codec, L, device, f, n=16_777_216, M=128, steps=100, gr
     k = kept_count(f, n)
     grads = make_grads(M, n, 0, device, torch)
     one = single_gradient(torch, codec, grads[0], k, n, graph=graph)
-XX
-    # 16 M than separate allocations (at 128 M 3 % slower: the headline keeps separate ones)
+    # slab_packets: the packets as rows of per-field slabs (codec.Packet.alloc_batch); its
+    # compaction is 2-3 % faster at 16 M, but the whole configs[2] step is not
+    # (profiles/r06_c2_slab_packets_ab.jsonl: 2.223-2.233 vs 2.220-2.230 ms), so off by default
     pkts = codec.Packet.alloc_batch(n, M, L.FC_FMT_IDXVAL, device, k=k) if slab_packets else \
         [codec.Packet.alloc(n, L.FC_FMT_IDXVAL, device, k=k) for _ in range(M)]
     w = [1.0 / M] * M
