@@ -501,12 +501,13 @@ def test_batch_encodes_on_concurrent_streams_stay_ok():
 
 @pytest.mark.timeout(120)
 def test_fused_encodes_on_concurrent_streams_never_stall():
-    """k_fused_mag (the lone packet and drop-in dense encodes) is a kernel whose workgroups wait
-    in-kernel, for the bracket of their own launch.  The library orders such launches per device
-    itself (include/fedcodec.h, Concurrency) — nothing in Python does any more — so two of them
-    (a packet encode and a dense one, their own workspaces) issued on two streams 200 times each,
-    with nothing else ordering them, never stall to the poll bound: every status is OK (counted
-    on each stream, no host sync) and both results equal the single-stream encodes'."""
+    """k_fused_mag (the lone packet and drop-in dense encodes, and fc_topk_encode_decode's
+    encode) is a kernel whose workgroups wait in-kernel, for the bracket of their own launch.
+    The library orders such launches per device itself (include/fedcodec.h, Concurrency) —
+    nothing in Python does any more — so a packet encode, a dense one and an encode + decode
+    (their own workspaces) issued on three streams 200 times each, with nothing else ordering
+    them, never stall to the poll bound: every status is OK (counted on each stream, no host
+    sync) and every result equals the single-stream calls'."""
     codec = _codec()
     assert not hasattr(codec, "_fused_encode")
     n, f = 1 << 24, 0.1
@@ -514,32 +515,39 @@ def test_fused_encodes_on_concurrent_streams_never_stall():
     g0 = torch.randn(n, device="cuda", generator=gen) * 1e-3
     g1 = torch.randn(n, device="cuda", generator=gen) * 3e-2
     k = co.effective_k(co.num_kept(f, n), n)
+    g2 = torch.randn(n, device="cuda", generator=gen)
     ref0 = _packet_bytes(codec.encode_top(g0, k))
     ref1 = codec.decode(codec.encode_top(g1, k)).clone()
-    s0, s1 = torch.cuda.Stream(), torch.cuda.Stream()
+    ref2p = codec.encode_top(g2, k)
+    ref2 = (_packet_bytes(ref2p), codec.decode(ref2p).clone())
+    s0, s1, s2 = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
     torch.cuda.synchronize()
     with torch.cuda.stream(s0):
         p0 = codec.encode_top(g0, k, check=False)
     with torch.cuda.stream(s1):
         p1 = codec.Packet.alloc(n, codec.L.FC_FMT_IDXVAL, g1.device, k=k)
         out1 = torch.empty_like(g1)
+    with torch.cuda.stream(s2):                 # fc_topk_encode_decode: its decode waits too
+        p2, out2 = codec.encode_decode_top(g2, k, check=False)
     torch.cuda.synchronize()
-    with torch.cuda.stream(s0):
-        bad0 = torch.zeros((), dtype=torch.int64, device="cuda")
-    with torch.cuda.stream(s1):
-        bad1 = torch.zeros((), dtype=torch.int64, device="cuda")
+    bad = [torch.zeros((), dtype=torch.int64, device="cuda") for _ in range(3)]
     torch.cuda.synchronize()
     for _ in range(200):                        # statuses counted on each stream, no host sync
         with torch.cuda.stream(s0):
             codec.encode_top(g0, k, packet=p0, check=False)
-            bad0 += (p0.hdr[36:40] != 0).any().to(torch.int64)
+            bad[0] += (p0.hdr[36:40] != 0).any().to(torch.int64)
         with torch.cuda.stream(s1):
             codec.compress_top_dense(g1, k, out=out1, packet=p1, check=False)
-            bad1 += (p1.hdr[36:40] != 0).any().to(torch.int64)
+            bad[1] += (p1.hdr[36:40] != 0).any().to(torch.int64)
+        with torch.cuda.stream(s2):
+            codec.encode_decode_top(g2, k, packet=p2, out=out2, check=False)
+            bad[2] += (p2.hdr[36:40] != 0).any().to(torch.int64)
     torch.cuda.synchronize()
-    assert int(bad0) == 0 and int(bad1) == 0
+    assert [int(b) for b in bad] == [0, 0, 0]
     assert _packet_bytes(p0) == ref0
     assert torch.equal(out1.view(torch.int32), ref1.view(torch.int32))
+    assert _packet_bytes(p2) == ref2[0]
+    assert torch.equal(out2.view(torch.int32), ref2[1].view(torch.int32))
 
 
 @pytest.mark.timeout(120)
