@@ -253,12 +253,17 @@ static PredArgs pred_args(const CompactArgs& a) {
   return p;
 }
 
-static int launch_compact_key(int key_mode, const CompactArgs& a, hipStream_t s, uint32_t m = 1) {
+// bin: a lone rand-k compaction also fills the candidate histogram (k_resolve<false> follows alone)
+static int launch_compact_key(int key_mode, const CompactArgs& a, hipStream_t s, uint32_t m = 1,
+                              bool bin = false) {
   TimedLaunch t(FC_TIME_COMPACT, s);
-  if (key_mode == FC_KEY_PHILOX)
-    hipLaunchKernelGGL((k_compact_pred<kSrcPhiloxKey, FC_FMT_IDXVAL>), dim3(a.nchunks, m), dim3(kCBlock), 0, s, pred_args(a));
-  else
+  if (key_mode == FC_KEY_PHILOX) {
+    PredArgs p = pred_args(a);
+    if (bin) p.chist = a.W.chist;
+    hipLaunchKernelGGL((k_compact_pred<kSrcPhiloxKey, FC_FMT_IDXVAL>), dim3(a.nchunks, m), dim3(kCBlock), 0, s, p);
+  } else {
     launch_compact_mag(a, m, s);
+  }
   FC_LAUNCHED("k_compact");
   return FC_OK;
 }
@@ -562,9 +567,10 @@ int fc_topk_encode(const float* g, uint64_t n, uint64_t k, int key_mode, uint64_
   else
     rc = launch_sample(key_mode, dim3(sgrid), g, P, seed, offset, ca.W, ca.ib, hdr, hi, nullptr, 0ull, s);
   if (rc) return rc;
-  rc = launch_compact_key(key_mode, ca, s);
+  const bool bin = key_mode == FC_KEY_PHILOX;   // rand-k bins its candidates while it compacts
+  rc = launch_compact_key(key_mode, ca, s, 1, bin);
   if (rc) return rc;
-  ra.rbin = 1;                       // the unfused compactions leave the binning to k_resolve
+  ra.rbin = bin ? 0 : 1;             // else the unfused compaction leaves the binning to k_resolve
   return launch_resolve(ra, s);
 }
 

@@ -80,6 +80,8 @@ struct PredArgs {
   const fc_encode_job* jobs; // batched rand-k: client blockIdx.y
   uint64_t ws_stride;
   uint32_t ib, nonfinite_keep;
+  uint32_t* chist;           // lone rand-k: the candidate histogram, binned here (one atomic per
+                             // candidate; k_resolve<false> then needs no binning launch)
 };
 
 __global__ __launch_bounds__(64) void k_write_hdr(fc_packet_hdr* hdr, HdrInit HI) {
@@ -124,13 +126,13 @@ __device__ __forceinline__ void pred_body(const PredArgs& a, uint32_t chunk, Pre
   }
 #define FC_LOC(q) (lbase + ((q) >> 2) * MagGeo<NW>::kIStride + ((q) & 3) * 64)
   // ---- predicates: bit q of pb (listed), cb (candidate), nb (NaN stand-in) ---------------
-  uint32_t Lk = 0, Li = 0, t_lo = 0, t_hi = 0, cand_on = 0;
+  uint32_t Lk = 0, Li = 0, t_lo = 0, t_hi = 0, cand_on = 0, sbin = 0;
   if (SRC == kSrcPhiloxKey) {
     const MagState st = mag_state(a.S);
     const bool none = st.L64 == kSelectNothing;
     Lk = none ? 0xffffffffu : (uint32_t)(st.L64 >> a.ib);
     Li = none ? 0xffffffffu : (uint32_t)(st.L64 & ((1ull << a.ib) - 1));
-    t_lo = st.t_lo; t_hi = st.t_hi; cand_on = st.cand_on;
+    t_lo = st.t_lo; t_hi = st.t_hi; cand_on = st.cand_on; sbin = st.sbin;
   }
   const uint64_t seg0 = ((uint64_t)base >> 8) + (uint32_t)w;
   uint32_t pb = 0, cb = 0, nb = 0;
@@ -229,7 +231,8 @@ __device__ __forceinline__ void pred_body(const PredArgs& a, uint32_t chunk, Pre
     }
   }
   // ---- candidates (rand-k): wave w's LDS sub-slot at a wave-uniform running count; the key
-  // is recomputed (one Philox block per segment that holds a candidate: rare) ---------------
+  // is recomputed (one Philox block per segment that holds a candidate: rare); a lone encode
+  // also bins them (a.chist) ---------------
   constexpr int kCW = kCandSlot / NW;
   uint32_t wc = 0;
   if (SRC == kSrcPhiloxKey && cand_on) {
@@ -243,10 +246,9 @@ __device__ __forceinline__ void pred_body(const PredArgs& a, uint32_t chunk, Pre
         const bool c = (cb >> q) & 1u;
         const uint64_t mc = __ballot(c);
         const uint32_t pos = wc + prefix_count(mc);
-        if (c && pos < (uint32_t)kCW) {
-          const uint32_t word = j == 0 ? r.x : j == 1 ? r.y : j == 2 ? r.z : r.w;
-          sh.cst[w * kCW + pos] = comp_of(word >> 1, base + FC_LOC(q), a.ib);
-        }
+        const uint32_t word = j == 0 ? r.x : j == 1 ? r.y : j == 2 ? r.z : r.w;
+        if (c && pos < (uint32_t)kCW) sh.cst[w * kCW + pos] = comp_of(word >> 1, base + FC_LOC(q), a.ib);
+        if (c && a.chist) atomicAdd(&a.chist[((word >> 1) - t_lo) >> sbin], 1u);
         wc += (uint32_t)__popcll(mc);
       }
     }

@@ -297,10 +297,11 @@ __device__ __forceinline__ FineWin pilot_window(const T* __restrict__ g, const S
   return win_of(s_out[2], s_out[0]);
 }
 
-// One launch: grid (ceil(nseg / kSampleSegs), clients).  k_sample1 has every workgroup compute
-// the window itself (no in-kernel wait); k_fused_mag's sample workgroups share workgroup 0's
-// (sc1 payload + flag; the others load their segments meanwhile): 256 workgroups re-reading the
-// same 32 KB pilot took ~7 us of loads.
+// One launch: grid (ceil(nseg / kSampleSegs), clients).  k_sample1 and (round 6) k_fused_mag
+// have every workgroup compute the window itself (no in-kernel wait); the shared form (workgroup
+// 0 publishes an sc1 payload the others poll; fc_topk_dense_f64_sampled's k_fused64) was
+// measured faster in round 4, when 256 workgroups re-reading the same 32 KB pilot took ~7 us of
+// loads, and 1-7 us slower in round 6 (profiles/r06_ab_fused_ownpilot.jsonl).
 struct SampleShared {
   uint32_t h[kHistBins];                          // pilot histogram, then the sample's
   uint32_t s_tmp[8], s_out[4], s_flag, s_win[3];
@@ -1153,7 +1154,11 @@ __device__ __forceinline__ void fused_mag_wg(const CompactArgs& a0, const Sample
   const uint32_t pub = sload2(&S->fz_seq).x + 1u;   // not written by this launch
   if (blockIdx.x < nsamp) {
     if (threadIdx.x >= kBlock) return;
-    sample_body<kKeyMag, true>(a0.g, P, 0ull, 0ull, a0.W, a0.ib, a0.hdr, HI, blockIdx.x, nsamp, true, u.s, pub);
+    // every sample workgroup computes the pilot window itself from the pilot segments (L2-hits
+    // after the first reader) instead of polling workgroup 0's published copy: the window is
+    // ready ~1.5 us sooner (encode_decode 16 M 59.0 -> 58.0 us, dense 128 M 209 -> 202 us;
+    // profiles/r06_ab_fused_ownpilot.jsonl)
+    sample_body<kKeyMag, false>(a0.g, P, 0ull, 0ull, a0.W, a0.ib, a0.hdr, HI, blockIdx.x, nsamp, false, u.s, pub);
     return;
   }
   // (chunks in dispatch order: spreading the resident ones over 8 / 64 address streams, as
