@@ -718,19 +718,30 @@ def test_rand_numpy_rng_golden(name):
     assert out.tobytes() == G.arr(name, "output").tobytes()
 
 
-@pytest.mark.parametrize("n,f", [(1000, 0.1), (100_003, 0.5), (3_000_001, 0.01)])
+@pytest.mark.parametrize("n,f", [(1000, 0.1), (100_003, 0.5), (3_000_001, 0.01), (24_581, 0.5),
+                                 (65_536, 0.9), (16_777_216, 0.1)])
 def test_rand_philox_matches_oracle(n, f):
+    """Native rand-k (fc_topk_encode with Philox keys): the lone encode bins its candidates in
+    the compaction (round 6) — its packet, header included, equals the batched encode's (whose
+    k_resolve<true> bins them) byte for byte, with no RETRY, and decodes to the oracle's choice.
+    24,581 at f = 0.5 overflows every full chunk's 256-entry candidate slot (~16 sigma = ~1,250
+    candidates over 4 chunks): the resolve re-reads those chunks' entries and recomputes keys."""
     codec = _codec()
     L = _L()
     g = np.random.default_rng(n).standard_normal(n, dtype=np.float32)
     k = co.num_kept(f, n)
     seed, off = 0xDEADBEEF12345, 7
-    pkt = codec.encode_top(torch.from_numpy(g).cuda(), k, key_mode=L.FC_KEY_PHILOX,
-                           seed=seed, offset=off)
+    gd = torch.from_numpy(g).cuda()
+    pkt = codec.encode_top(gd, k, key_mode=L.FC_KEY_PHILOX, seed=seed, offset=off)
+    assert pkt.header().status == 0
     out = codec.decode(pkt).cpu().numpy()
     keys = (ph.element_words(n, seed, off) >> np.uint32(1)).astype(np.uint32)
     want = po.selected_indices(keys, k)
     assert out.tobytes() == po.decode_dense(n, want, g[want]).tobytes()
+    if 0 < k < n:
+        (bp,) = codec.encode_top_batch([gd], k, key_mode=L.FC_KEY_PHILOX, seeds=[seed], offsets=[off])
+        assert _packet_bytes(bp) == _packet_bytes(pkt)
+        assert bp.hdr.cpu().numpy().tobytes() == pkt.hdr.cpu().numpy().tobytes()
 
 
 # ---- dropout ---------------------------------------------------------------------------
