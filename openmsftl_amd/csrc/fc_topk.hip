@@ -1028,6 +1028,7 @@ __device__ __forceinline__ void compact_mag_item(const CompactArgs& a0, const Ma
 
 constexpr int FC_MAG1_WAVES_PER_EU = 8;
 constexpr int FC_MAG1_IL = 64;
+constexpr int FC_FUSED_SREC = 2048;       // first chunk of k_fused_mag<false> that tries the scalar record
 // Dispatch order: workgroups are dispatched x-fastest, so the chunks of FC_MAG1_IL clients are
 // interleaved (chunk-major within a group of clients): FC_MAG1_IL address streams are in
 // flight at once instead of one.  Measured (tools/kbench.py --batch 64, 128 M floats): IL 1 / 4
@@ -1170,11 +1171,28 @@ __device__ __forceinline__ void fused_mag_wg(const CompactArgs& a0, const Sample
   // arrive long before the bracket (~14 us at 16 M).  16 M dense fused kernel 38.7 -> 37.6 us,
   // 128 M packet 140.5 -> 138 us (profiles/r05_ab_fused_publish_find_delay.jsonl)
   if (chunk < 1024u) __builtin_amdgcn_s_sleep(90);
+  // Later resident rounds of the packet form (chunk >= FC_FUSED_SREC, long after the bracket
+  // is out) read the record with a SCALAR load issued before their gradient loads: it has its
+  // own queue, while the sc1 poll's load waits behind the wave's 16 vector loads, and a matching
+  // tag skips the poll and its barrier.  A stale or unpublished copy (a compute unit's scalar
+  // cache or an XCD's L2 holding the line from before the publication) only falls back to the
+  // poll.  128 M encode 154.6 -> 147.8 us, encode_decode 246.6 -> 239.2 us on one box; the dense
+  // form got 8 us SLOWER with it (138 spilled SGPRs there), so it keeps the poll
+  // (profiles/r06_ab_fused_scalar_record.jsonl).
+  const uint32_t* rec = &a0.W.pub[(blockIdx.x % kPubCopies) * kPubStride];
+  const uint32_t tag = pub | 0x80000000u;
+  typedef __attribute__((address_space(4))) const fc_rec4 fc_crec4;
+  const bool try_s = !DENSE && chunk >= (uint32_t)FC_FUSED_SREC;
+  fc_rec4 sr = {0u, 0u, 0u, 0u};
+  if (try_s) sr = *(fc_crec4*)rec;
   mag_load<NW>(a0.g, chunk, a0.n, x);
   FC_TR(24);
+  MagState st;
+  if (try_s && sr.w == tag) {
+    st.t_lo = sr.x; st.t_hi = sr.y; st.sbin = sr.z; st.cand_on = 1u;
+    st.L64 = (uint64_t)sr.x << a0.ib;   // = the sample's L64
+  } else {
   if (threadIdx.x == 0) {           // this workgroup's copy of the bracket record
-    const uint32_t* rec = &a0.W.pub[(blockIdx.x % kPubCopies) * kPubStride];
-    const uint32_t tag = pub | 0x80000000u;
     uint32_t it = 0;
     fc_rec4 r = ld16_agent(rec);
     while (r.w != tag && ++it < kSpinMax) {
@@ -1189,7 +1207,8 @@ __device__ __forceinline__ void fused_mag_wg(const CompactArgs& a0, const Sample
   }
   __syncthreads();
   FC_TR(25);
-  const MagState st = s_st;
+  st = s_st;
+  }
   compact_mag_item<NW, MagShared, DENSE, true, !DENSE>(a0, mag_out(a0, 0u), chunk, st, x, u.m);
   FC_TR(26);
 }
