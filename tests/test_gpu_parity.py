@@ -1247,10 +1247,10 @@ def test_batched_compaction_past_the_grid_y_limit():
 
 @pytest.mark.timeout(120)
 def test_graphed_calls_equal_eager_calls():
-    """codec.GraphedCalls: the lone packet encode + decode, the drop-in dense encode and a
-    batched encode + fold, captured into one HIP graph and replayed three times, give the eager
-    calls' bytes (the fused kernels' bracket tags and every self-cleaning counter live on the
-    device, so replays line up with eager calls)."""
+    """codec.GraphedCalls: the lone packet encode + decode, fc_topk_encode_decode, a native
+    rand-k encode, the drop-in dense encode and a batched encode + fold, captured into one HIP
+    graph and replayed three times, give the eager calls' bytes (the fused kernels' bracket tags
+    and every self-cleaning counter live on the device, so replays line up with eager calls)."""
     codec = _codec()
     from openmsftl_amd import _lib as L
     n, M, f = 3_000_017, 6, 0.1
@@ -1272,19 +1272,31 @@ def test_graphed_calls_equal_eager_calls():
     views = codec.views_tensor(pk, w, dev)
     acc = torch.empty(n, dtype=torch.float32, device=dev)
 
+    ref_ed = codec.encode_decode_top(grads[2], k)
+    ref_ed = (_packet_bytes(ref_ed[0]), ref_ed[1].clone())
+    ref_rk = _packet_bytes(codec.encode_top(grads[3], k, key_mode=L.FC_KEY_PHILOX, seed=3, offset=9))
+    epkt = codec.Packet.alloc(n, L.FC_FMT_IDXVAL, dev, k=k)
+    eout = torch.empty(n, dtype=torch.float32, device=dev)
+    rpkt = codec.Packet.alloc(n, L.FC_FMT_IDXVAL, dev, k=k)
+
     def calls():
         codec.encode_top(grads[0], k, packet=pkt, check=False)
         codec.decode(pkt, out=out)
+        codec.encode_decode_top(grads[2], k, packet=epkt, out=eout, check=False)
+        codec.encode_top(grads[3], k, key_mode=L.FC_KEY_PHILOX, seed=3, offset=9, packet=rpkt, check=False)
         codec.compress_top_dense(grads[1], k, out=dense, packet=dpkt, check=False)
         codec.encode_top_batch(grads, k, packets=pk, jobs=jobs, check=False)
         codec.decode_accumulate(pk, w, out=acc, views=views)
 
     gc = codec.GraphedCalls(calls)
     for _ in range(3):
-        out.zero_(); dense.zero_(); acc.zero_()
+        out.zero_(); dense.zero_(); acc.zero_(); eout.zero_()
         gc.replay()
         torch.cuda.synchronize()
         assert codec.resolve([pkt]) == 0 and codec.resolve(pk) == 0
+        assert codec.resolve([epkt]) == 0 and codec.resolve([rpkt]) == 0
+        assert _packet_bytes(epkt) == ref_ed[0] and torch.equal(eout.view(torch.int32), ref_ed[1].view(torch.int32))
+        assert _packet_bytes(rpkt) == ref_rk
         assert dpkt.header().status == 0
         assert _packet_bytes(pkt) == ref_pkt
         assert torch.equal(dense.view(torch.int32), ref_dense.view(torch.int32))
