@@ -61,6 +61,15 @@ def _cluster_bounds(m: int, cluster_size: int):
     return bounds
 
 
+def _merge_log(stage: int, cluster_size: int, bounds) -> None:
+    """The reference's progress lines for one merge stage (aggregation.py:71, 88, 90), text and
+    order included."""
+    print("{}-stage gradient aggregation: cluster size={}".format(stage, cluster_size))
+    print("#client clusters: {}".format(len(bounds)))
+    for s, e in bounds:
+        print("Averaging gradient from the {}-th client to the {}=th".format(s, e))
+
+
 def _device_of(agg) -> torch.device:
     dev = getattr(agg, "device", None)
     if isinstance(dev, torch.device) and dev.type == "cuda":
@@ -288,6 +297,7 @@ def merge_streamed(agg, clients, n: int, plan: RowPlan, cluster_size: int,
     """First merge stage straight from the streamed rows (aggregation.py:80-93): each
     cluster's +0-started row-order sum (weights 1), then one fl32 division by its size."""
     bounds = _cluster_bounds(len(clients), cluster_size)
+    _merge_log(0, cluster_size, bounds)
     H = torch.empty((len(bounds), n), dtype=torch.float32, device=dev)
     for r, (s, e) in enumerate(bounds):
         row = torch.empty(n, dtype=torch.float32, device=dev)   # 16-B aligned while written
@@ -296,11 +306,12 @@ def merge_streamed(agg, clients, n: int, plan: RowPlan, cluster_size: int,
     return H
 
 
-def merge_stages(G: torch.Tensor, sizes) -> torch.Tensor:
+def merge_stages(G: torch.Tensor, sizes, first_stage: int = 0) -> torch.Tensor:
     """Merge stages over dense device rows (fp32 or fp64 G): +0-started sums (weights 1),
     then / count, in G's dtype (np.mean(G[s:e], axis=0), aggregation.py:91)."""
-    for cs in sizes:
+    for i, cs in enumerate(sizes):
         bounds = _cluster_bounds(G.shape[0], cs)
+        _merge_log(first_stage + i, cs, bounds)
         rows = []
         for s, e in bounds:
             r = codec.weighted_sum_dense(G[s:e], torch.ones(e - s, dtype=G.dtype), out_dtype=G.dtype)
@@ -375,7 +386,7 @@ def aggregate_grads(self, clients: List, input_feature: np.ndarray = None,
             try:
                 if self.num_hierarchies > 0:
                     H = merge_streamed(self, clients, n, plan, self.cluster_size_list[0], dev)
-                    H = merge_stages(H, self.cluster_size_list[1:])
+                    H = merge_stages(H, self.cluster_size_list[1:], first_stage=1)
                     self.curr_G = H
                     agg = self.gar.aggregate(G=H, client_ids=np.arange(H.shape[0]))
                 else:

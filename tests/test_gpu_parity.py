@@ -1018,11 +1018,26 @@ def test_aggregator_hierarchical_golden(name):
     assert agg.agg_grad.tobytes() == A.arr(name, "output").tobytes()
 
 
+def _ref_merge_lines(m, sizes):
+    """The progress lines the reference prints for its merge stages (aggregation.py:71, 88, 90)."""
+    out = []
+    for stage, cs in enumerate(sizes):
+        num = m // cs
+        b = [[i * cs, (i + 1) * cs] for i in range(num)]
+        b[-1][1] = max(b[-1][1], m)
+        out.append(f"{stage}-stage gradient aggregation: cluster size={cs}")
+        out.append(f"#client clusters: {num}")
+        out += [f"Averaging gradient from the {s}-th client to the {e}=th" for s, e in b]
+        m = num
+    return out
+
+
 @pytest.mark.parametrize("sizes", [[], [3], [4, 2]])
-def test_aggregator_top_packets_match_dense_reference(sizes):
+def test_aggregator_top_packets_match_dense_reference(sizes, capsys):
     """The streamed packet path (host ring -> top-k encode -> packet fold / packet cluster
     means) == the dense G the reference builds from the same compressed rows, merged and
-    reduced (oracle).  A budget of a few packets forces several fold groups per cluster."""
+    reduced (oracle).  A budget of a few packets forces several fold groups per cluster.  The
+    merge stages print the reference's progress lines."""
     from openmsftl_amd.aggregation import Aggregator
     M, n, f = 17, 40_961, 0.1
     rng = np.random.default_rng(len(sizes))
@@ -1036,8 +1051,10 @@ def test_aggregator_top_packets_match_dense_reference(sizes):
     agg = Aggregator({"aggregation_scheme": "fed_avg", "num_hierarchies": len(sizes),
                       "cluster_size_list": sizes,
                       "device_budget_bytes": 6 * 4 * n + 3 * packet_bytes(n) + (8 << 20)})
+    capsys.readouterr()
     agg.aggregate_grads(clients)
     assert agg.agg_path == "stream"                # the streamed packet path ran
+    assert capsys.readouterr().out.splitlines() == _ref_merge_lines(M, sizes)
     Gd = go.build_dense_G([co.compress(cfg, x) for x in grads], np.float32)
     for cs in sizes:
         Gd = go.merge_gradient(Gd, cs)
