@@ -30,7 +30,7 @@
  * (fc_topk_encode with key_mode MAGNITUDE and 0 < k < n, fc_topk_encode_dense) and k_fused64
  * (fc_topk_dense_f64_sampled).  Two of them on two streams of one device could stall each other
  * (each XCD dispatches the two grids in its own order), so the library queues each one after the
- * device's previous one: an event it owns is recorded after every such launch, and a launch on
+ * device's previous one: an event it owns completes with every such launch, and a launch on
  * another stream first waits for it.  A launch into a stream being captured (hipGraph) is not
  * ordered; bracket the graph's launch with fc_fused_order_begin / fc_fused_order_end.  All other
  * kernels synchronise only through last-arriver tickets (no workgroup waits for another).

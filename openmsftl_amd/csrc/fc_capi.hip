@@ -12,6 +12,8 @@
 
 // Part of the unity build (fedcodec.hip): the kernels and their argument structs from
 // fc_topk.hip / fc_decode.hip are visible here.
+#include <hip/hip_ext.h>
+
 #include "fc_state.h"
 
 using namespace fc;
@@ -362,9 +364,14 @@ class FusedGuard {
     }
     if (F_->pending && F_->last != s) (void)hipStreamWaitEvent(s, F_->ev, 0);
   }
+  // The launch may carry the ordering event itself (hipExtLaunchKernelGGL's stop event: the
+  // kernel's own completion signal): a separate hipEventRecord after the kernel put one more
+  // packet between consecutive launches, ~3 us per call (profiles/r06_ab_fused_order_event.jsonl).
+  hipEvent_t stop_event() const { return F_ ? F_->ev : nullptr; }
+  void recorded() { rec_ = true; }
   ~FusedGuard() {
     if (!F_) return;
-    (void)hipEventRecord(F_->ev, s_);
+    if (!rec_) (void)hipEventRecord(F_->ev, s_);
     F_->last = s_;
     F_->pending = true;
     F_->mu.unlock();
@@ -375,6 +382,7 @@ class FusedGuard {
  private:
   hipStream_t s_;
   FusedOrder* F_ = nullptr;
+  bool rec_ = false;
 };
 }  // namespace
 
@@ -410,9 +418,11 @@ static int launch_fused(const CompactArgs& ca, const SamplePlan& P, const HdrIni
   FusedGuard order(s);
   TimedLaunch t(FC_TIME_COMPACT, s);
   const dim3 grid(nsamp + ca.nchunks);
-  if (ca.dense) hipLaunchKernelGGL(k_fused_mag<true>, grid, dim3(kCBlock), 0, s, ca, P, hi, nsamp);
-  else hipLaunchKernelGGL(k_fused_mag<false>, grid, dim3(kCBlock), 0, s, ca, P, hi, nsamp);
+  const hipEvent_t ev = order.stop_event();       // null while capturing: a plain launch
+  if (ca.dense) hipExtLaunchKernelGGL(k_fused_mag<true>, grid, dim3(kCBlock), 0, s, nullptr, ev, 0, ca, P, hi, nsamp);
+  else hipExtLaunchKernelGGL(k_fused_mag<false>, grid, dim3(kCBlock), 0, s, nullptr, ev, 0, ca, P, hi, nsamp);
   FC_LAUNCHED("k_fused_mag");
+  if (ev) order.recorded();
   return FC_OK;
 }
 
@@ -1010,8 +1020,10 @@ int fc_topk_dense_f64_sampled(const double* g, uint64_t n, uint64_t k, double* o
     TimedLaunch t(FC_TIME_COMPACT, s);
     const uint32_t nsamp = (P.nseg + P.segs - 1) / P.segs;
     FusedGuard order(s);
-    hipLaunchKernelGGL(k_fused64, dim3(nsamp + a.nchunks), dim3(kBlock), 0, s, a, P, W, ib, hdr, hi, nsamp);
+    const hipEvent_t ev = order.stop_event();
+    hipExtLaunchKernelGGL(k_fused64, dim3(nsamp + a.nchunks), dim3(kBlock), 0, s, nullptr, ev, 0, a, P, W, ib, hdr, hi, nsamp);
     FC_LAUNCHED("k_fused64");
+    if (ev) order.recorded();
   }
   {
     TimedLaunch t(FC_TIME_ENGINE, s);
