@@ -934,27 +934,32 @@ struct DecResArgs {
 __global__ __launch_bounds__(kQBlock, 4) void k_decode_res(DecResArgs a) {
   __shared__ __attribute__((aligned(16))) float tile[kChunk];    // the finisher: its sort list
   __shared__ uint32_t s_skip[4][kQuarter / 32];                 // bin-beta locations per quarter
-  __shared__ uint32_t s_last;
+  __shared__ uint32_t s_fin[4];                                 // per wave: it holds the finisher
   __shared__ uint64_t s_T;
   const int tid = threadIdx.x, lane = lane_id();
   const int q = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t c = blockIdx.x;
   const uint64_t base = (uint64_t)c * kChunk;
   const uint32_t qbase = (uint32_t)base + (uint32_t)(q * kQuarter);
+  // the quarter offsets with the state: one round trip for both (the offsets used to be loaded
+  // only after the flags were known and a workgroup barrier)
+  const uint64_t qo = a.qoff[c];
   TopkState* S = a.W.st;
   const uint32_t t_lo = S->t_lo, t_hi = S->t_hi, sbin = S->sbin;
   const uint32_t beta = S->rb_beta, flags = S->rb_flags, cnt = S->rb_cnt;
   const bool gather = (flags & 3u) == 0;                         // not retry, not rank 0
+  // every wave owns its quarter of the tile, its skip bits and its finisher flag: no barrier
+  // before the entries (a wave's LDS stores land in program order)
   float* qt = tile + q * kQuarter;
 #pragma unroll
   for (int i = 0; i < kQuarter / 256; ++i)
     *reinterpret_cast<float4*>(&qt[i * 256 + lane * 4]) = make_float4(0.f, 0.f, 0.f, 0.f);
   s_skip[q][lane] = 0u;
-  if (tid == 0) s_last = 0u;
-  __syncthreads();
+  if (lane == 0) s_fin[q] = 0u;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
   bool finisher = false;
   if (!(flags & 1u)) {
-    const uint64_t qo = a.qoff[c];
     const uint32_t st = q == 0 ? 0u : (uint32_t)(qo >> (16 * (q - 1))) & 0xffffu;
     const uint32_t en = q == 3 ? (uint32_t)(qo >> 48) : (uint32_t)(qo >> (16 * q)) & 0xffffu;
     gu16* pidx = (gu16*)a.idx + base;
@@ -978,7 +983,7 @@ __global__ __launch_bounds__(kQBlock, 4) void k_decode_res(DecResArgs a) {
       }
     }
   }
-  if (finisher) s_last = 1u;
+  if (finisher) s_fin[q] = 1u;
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   __builtin_amdgcn_wave_barrier();
   float* out = a.out;
@@ -999,7 +1004,7 @@ __global__ __launch_bounds__(kQBlock, 4) void k_decode_res(DecResArgs a) {
   }
   if (!gather) return;                                           // uniform
   __syncthreads();
-  if (!s_last) return;
+  if (!(s_fin[0] | s_fin[1] | s_fin[2] | s_fin[3])) return;
   // ---- the finisher: T64 = the r_in-th largest of bin beta, its locations, the header ----
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   uint64_t* sv = reinterpret_cast<uint64_t*>(tile);               // 4096 comps
