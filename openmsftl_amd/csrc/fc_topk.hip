@@ -151,7 +151,7 @@ constexpr int kSampleSegs = FC_SAMPLE_SEGS_PER_WG;
 // Bounded in-kernel polls (k_fused_mag's bracket and window waits, ~0.25 us each): a bracket
 // arrives in 14-30 us (~100 polls); 8192 polls (~2-4 ms) end a co-residency stall between two
 // fused launches on two queues with a RETRY (the exact re-encode) instead of ~60 ms
-// (tests/test_gpu_parity.py::test_fused_encodes_on_concurrent_streams_are_bounded).
+// (tests/test_gpu_parity.py::test_fused_encodes_on_concurrent_streams_never_stall).
 constexpr uint32_t kSpinMax = 1u << 13;
 constexpr uint32_t kFineLo = 1024, kFineBins = 2048, kFineHi = kFineLo + kFineBins;
 constexpr uint32_t kCoarseShift = 21;            // 0x7fffffff >> 21 = 1023
