@@ -4,8 +4,8 @@
 set -o pipefail
 PART=${1:-a}
 if [ "$PART" = a ]; then
-  SKIP_PROF=1 SKIP_PMC=1 bash tools/r06_round.sh r06c
+  SKIP_PROF=1 SKIP_PMC=1 bash tools/r06_round.sh ${TAG:-r06c}
 else
-  SKIP_TESTS=1 SKIP_BENCH=1 SKIP_PMC=1 bash tools/r06_round.sh r06c &&
+  SKIP_TESTS=1 SKIP_BENCH=1 SKIP_PMC=1 bash tools/r06_round.sh ${TAG:-r06c} &&
   bash tools/pmc_r06.sh r06c_pmc > gpurun_out/r06c_pmc.log 2>&1
 fi
