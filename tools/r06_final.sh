@@ -7,5 +7,5 @@ if [ "$PART" = a ]; then
   SKIP_PROF=1 SKIP_PMC=1 bash tools/r06_round.sh ${TAG:-r06c}
 else
   SKIP_TESTS=1 SKIP_BENCH=1 SKIP_PMC=1 bash tools/r06_round.sh ${TAG:-r06c} &&
-  bash tools/pmc_r06.sh r06c_pmc > gpurun_out/r06c_pmc.log 2>&1
+  bash tools/pmc_r06.sh ${TAG:-r06c}_pmc > gpurun_out/${TAG:-r06c}_pmc.log 2>&1
 fi
