@@ -615,7 +615,7 @@ def dense_moved_bytes(n, pkt):
 
 
 def small_configs(torch, codec, L, device, f, n=16_777_216, M=128, steps=100, graph=True,
-                  slab_packets=False):
+                  slab_packets=False, streams=1, pipeline=False):
     """BASELINE configs[1] (one 16 M gradient: encode + dense decode) and configs[2] (128
     clients x 16 M: batched encode + on-device FedAVG fold), device-resident, same codec."""
     from openmsftl_amd.compression import kept_count
@@ -633,7 +633,11 @@ def small_configs(torch, codec, L, device, f, n=16_777_216, M=128, steps=100, gr
     acc = torch.empty(n, dtype=torch.float32, device=device)
 
     def step():
-        codec.encode_top_batch(grads, k, packets=pkts, jobs=jobs, check=False)
+        if pipeline:                    # each sub-batch folded on its stream once encoded
+            codec.encode_fold_batch(grads, k, w, acc, packets=pkts, jobs=jobs, views=views,
+                                    streams=streams)
+            return
+        codec.encode_top_batch(grads, k, packets=pkts, jobs=jobs, check=False, streams=streams)
         codec.decode_accumulate(pkts, w, out=acc, views=views)
 
     for _ in range(10):                 # 2.4 ms steps: warm enough that clocks have settled
@@ -651,7 +655,7 @@ def small_configs(torch, codec, L, device, f, n=16_777_216, M=128, steps=100, gr
                                 "grad_GBps": round(4.0 * n * M / dt / 1e9, 1),
                                 "alg_GBps": round(alg / dt / 1e9, 1),
                                 "hbm_frac": round(alg / dt / 1e9 / HBM_PEAK_GBPS, 4),
-                                "exact_fallbacks": redo}}
+                                "exact_fallbacks": redo, "streams": streams, "pipeline": pipeline}}
 
 
 def _time_us(torch, fn, iters=20, warm=3):

@@ -15,6 +15,8 @@ def main():
     ap.add_argument("--tag", default="")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--separate-packets", action="store_true")
+    ap.add_argument("--streams", type=int, default=1)
+    ap.add_argument("--pipeline", action="store_true")
     args = ap.parse_args()
     import torch
     from openmsftl_amd import _lib as L
@@ -23,7 +25,8 @@ def main():
     from openmsftl_amd import codec
     import bench
     r = bench.small_configs(torch, codec, L, torch.device("cuda", 0), 0.1, steps=args.steps,
-                           slab_packets=not args.separate_packets)
+                           slab_packets=not args.separate_packets, streams=args.streams,
+                           pipeline=args.pipeline)
     c1, c2 = r["config1_single_16M"], r["config2_128x16M"]
     print(json.dumps({"tag": args.tag, "slab_packets": not args.separate_packets, "c2_ms": c2["ms_per_step"], "c2_frac": c2["hbm_frac"],
                       "c1_dense_us": c1["fused_dense"]["us"], "c1_rt_us": c1["us_per_encode_decode"]}),
