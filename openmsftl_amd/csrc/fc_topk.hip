@@ -803,6 +803,8 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
     for (int q = 0; q < NQ; ++q) {
       const bool c = mag_cand<FAST>(P, x[q]);
       const uint64_t mc = __ballot(c);
+      if (mc == 0) continue;   // uniform: most groups hold no candidate (configs[2] -1.3 %,
+                               // profiles/r06_ab_cand_skip.jsonl)
       const uint32_t pos = wc + prefix_count(mc);
       if (c) {
         const uint32_t e = base + FC_LOC(q);
