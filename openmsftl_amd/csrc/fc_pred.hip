@@ -106,6 +106,7 @@ __device__ __forceinline__ void pred_body(const PredArgs& a, uint32_t chunk, Pre
   constexpr int NW = kCWaves, NQ = MagGeo<NW>::kQ, NI = NQ / 4;
   static_assert(NQ == 16, "16 elements per lane");
   const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  const int wu = __builtin_amdgcn_readfirstlane(w);     // uniform: the readlane index below
   const uint32_t base = chunk * (uint32_t)kChunk;
   const uint32_t n32 = (uint32_t)a.n;
   const uint32_t lbase = (uint32_t)(w * 256 + lane);
@@ -207,7 +208,7 @@ __device__ __forceinline__ void pred_body(const PredArgs& a, uint32_t chunk, Pre
   const uint32_t e3 = e2 + ((word >> 16) & 0xffu);
   const uint32_t o01 = e0 | (e1 << 16), o23 = e2 | (e3 << 16);
   auto goff_of = [&](int q) -> uint32_t {
-    const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)((q & 2) ? o23 : o01), (q >> 2) * NW + w);
+    const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)((q & 2) ? o23 : o01), (q >> 2) * NW + wu);
     return (q & 1) ? v >> 16 : v & 0xffffu;
   };
   // ---- phase 2: listed entries -> LDS stage (or straight to the slot); bitmap words -------

@@ -703,6 +703,7 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
                                                  float (&x)[MagGeo<NW>::kQ], SH& sh,
                                                  uint32_t chunk, uint32_t sbin) {
   const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  const int wu = __builtin_amdgcn_readfirstlane(w);     // uniform: the readlane index below
   const uint32_t base = chunk * (uint32_t)kChunk;
   const uint32_t lbase = (uint32_t)(w * 256 + lane);
   constexpr int NQ = MagGeo<NW>::kQ, NI = NQ / 4;
@@ -744,7 +745,7 @@ __device__ __forceinline__ void compact_mag_body(const MagOut& a, const MagPred&
   // group q's slot offset, read from its holder lane where it is used (a precomputed array
   // is NQ live SGPRs: it spilled at NQ = 32)
   auto goff_of = [&](int q) -> uint32_t {
-    const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)((q & 2) ? o23 : o01), (q >> 2) * NW + w);
+    const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)((q & 2) ? o23 : o01), (q >> 2) * NW + wu);
     return (q & 1) ? v >> 16 : v & 0xffffu;
   };
 
